@@ -1,0 +1,298 @@
+// gb_context.cpp -- library context: init/finalize, the HIP stream, the
+// stream-ordered device memory pool, error plumbing, descriptors, builtin
+// object lookup.  (Replaces SuiteSparse's GrB_init / GxB_Global / GrB_Descriptor
+// surface used by reference graphblas/__init__.py:118-197 and
+// core/descriptor.py:92-156.)
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+
+#include "gb_internal.h"
+
+namespace {
+bool g_init = false;
+int g_device = 0;
+hipStream_t g_own_stream = nullptr;
+hipStream_t g_user_stream = nullptr;
+bool g_user_stream_set = false;
+std::mutex g_knob_mu;
+std::map<std::string, int64_t> g_knobs;
+}  // namespace
+
+static const GrB_Index GB_ALL_SENTINEL = 0;
+extern "C" {
+const GrB_Index *GrB_ALL = &GB_ALL_SENTINEL;
+}
+
+[[noreturn]] void gb_throw(GrB_Info info, const std::string &msg) { throw gb_exception{info, msg}; }
+
+void gb_hip_check(hipError_t e, const char *what) {
+    if (e == hipSuccess) return;
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {
+        (void)hipGetLastError();
+        gb_throw(GrB_OUT_OF_MEMORY, std::string("device out of memory: ") + what);
+    }
+    gb_throw(GrB_PANIC, std::string("HIP error ") + hipGetErrorString(e) + " in " + what);
+}
+
+static void gb_do_init() {
+    if (g_init) return;
+    const char *dev = getenv("GRAPHBLAS_AMD_DEVICE");
+    if (dev) g_device = atoi(dev);
+    GB_HIP(hipSetDevice(g_device));
+    GB_HIP(hipStreamCreateWithFlags(&g_own_stream, hipStreamNonBlocking));
+    // keep freed blocks in the pool (no release to the OS between calls)
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, g_device) == hipSuccess) {
+        uint64_t thr = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+    }
+    g_init = true;
+}
+
+void gb_require_init() {
+    if (!g_init) gb_do_init();  // lazy init, like python-graphblas's auto-init
+}
+
+hipStream_t gb_stream() {
+    gb_require_init();
+    return g_user_stream_set ? g_user_stream : g_own_stream;
+}
+
+void gb_sync() { GB_HIP(hipStreamSynchronize(gb_stream())); }
+
+int64_t gb_knob(const char *key) {
+    std::lock_guard<std::mutex> lk(g_knob_mu);
+    auto it = g_knobs.find(key);
+    return it == g_knobs.end() ? 0 : it->second;
+}
+
+void *gb_malloc(size_t bytes) {
+    void *p = nullptr;
+    if (bytes == 0) bytes = 16;
+    bytes = (bytes + 255) & ~(size_t)255;
+    hipError_t e = hipMallocAsync(&p, bytes, gb_stream());
+    if (e != hipSuccess || !p) {
+        (void)hipGetLastError();
+        gb_throw(GrB_OUT_OF_MEMORY, "device allocation of " + std::to_string(bytes) + " bytes failed");
+    }
+    return p;
+}
+
+void gb_free(void *p) {
+    if (p) (void)hipFreeAsync(p, gb_stream());
+}
+
+void gb_memset(void *p, int v, size_t bytes) {
+    if (bytes) GB_HIP(hipMemsetAsync(p, v, bytes, gb_stream()));
+}
+void gb_copy_d2d(void *dst, const void *src, size_t bytes) {
+    if (bytes) GB_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, gb_stream()));
+}
+void gb_copy_h2d(void *dst, const void *src, size_t bytes) {
+    if (bytes) GB_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, gb_stream()));
+}
+void gb_copy_d2h(void *dst, const void *src, size_t bytes) {
+    if (bytes) GB_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, gb_stream()));
+    gb_sync();
+}
+int64_t gb_read_i64(const int64_t *dptr) {
+    int64_t v = 0;
+    gb_copy_d2h(&v, dptr, sizeof(v));
+    return v;
+}
+
+static const char *k_type_names[] = {"BOOL", "INT8", "UINT8", "INT16", "UINT16", "INT32",
+                                     "UINT32", "INT64", "UINT64", "FP32", "FP64"};
+static const size_t k_type_sizes[] = {1, 1, 1, 2, 2, 4, 4, 8, 8, 4, 8};
+const char *gb_type_name(int code) { return k_type_names[code]; }
+size_t gb_type_size(int code) { return k_type_sizes[code]; }
+GrB_Type gb_type_of(int code) {
+    switch (code) {
+    case GBAMD_T_BOOL: return GrB_BOOL;
+    case GBAMD_T_INT8: return GrB_INT8;
+    case GBAMD_T_UINT8: return GrB_UINT8;
+    case GBAMD_T_INT16: return GrB_INT16;
+    case GBAMD_T_UINT16: return GrB_UINT16;
+    case GBAMD_T_INT32: return GrB_INT32;
+    case GBAMD_T_UINT32: return GrB_UINT32;
+    case GBAMD_T_INT64: return GrB_INT64;
+    case GBAMD_T_UINT64: return GrB_UINT64;
+    case GBAMD_T_FP32: return GrB_FP32;
+    default: return GrB_FP64;
+    }
+}
+
+gb_desc gb_read_desc(const GrB_Descriptor d) {
+    gb_desc r;
+    if (!d) return r;
+    GB_REQUIRE(d->magic == GB_MAGIC, GrB_UNINITIALIZED_OBJECT, "invalid descriptor");
+    r.replace = d->outp == GrB_REPLACE;
+    r.comp = (d->mask & GrB_COMP) != 0;
+    r.structure = (d->mask & GrB_STRUCTURE) != 0;
+    r.tran0 = d->inp0 == GrB_TRAN;
+    r.tran1 = d->inp1 == GrB_TRAN;
+    return r;
+}
+
+extern "C" {
+
+GrB_Info GrB_init(GrB_Mode mode) {
+    (void)mode;
+    return gb_api(nullptr, [&] {
+        GB_REQUIRE(!g_init, GrB_INVALID_VALUE, "GrB_init called twice");
+        gb_do_init();
+    });
+}
+
+GrB_Info GrB_finalize(void) {
+    return gb_api(nullptr, [&] {
+        if (!g_init) return;
+        GB_HIP(hipDeviceSynchronize());
+    });
+}
+
+GrB_Info GrB_getVersion(unsigned int *version, unsigned int *subversion) {
+    if (!version || !subversion) return GrB_NULL_POINTER;
+    *version = GRB_VERSION;
+    *subversion = GRB_SUBVERSION;
+    return GrB_SUCCESS;
+}
+
+GrB_Info GxB_Context_set_stream(void *hip_stream) {
+    return gb_api(nullptr, [&] {
+        gb_require_init();
+        g_user_stream = (hipStream_t)hip_stream;
+        g_user_stream_set = hip_stream != nullptr;
+    });
+}
+
+GrB_Info GxB_Context_get_stream(void **hip_stream) {
+    if (!hip_stream) return GrB_NULL_POINTER;
+    return gb_api(nullptr, [&] { *hip_stream = (void *)gb_stream(); });
+}
+
+GrB_Info GxB_Context_set_device(int device) {
+    if (g_init) return GrB_INVALID_VALUE;
+    g_device = device;
+    return GrB_SUCCESS;
+}
+
+GrB_Info GxB_Global_set_int(const char *key, int64_t value) {
+    if (!key) return GrB_NULL_POINTER;
+    std::lock_guard<std::mutex> lk(g_knob_mu);
+    g_knobs[key] = value;
+    return GrB_SUCCESS;
+}
+
+GrB_Info GxB_Global_get_int(const char *key, int64_t *value) {
+    if (!key || !value) return GrB_NULL_POINTER;
+    *value = gb_knob(key);
+    return GrB_SUCCESS;
+}
+
+GrB_Info GxB_builtin_lookup(void **handle, int *kind, const char *name) {
+    if (!handle || !kind || !name) return GrB_NULL_POINTER;
+    static std::map<std::string, const GB_builtin_entry *> *idx = nullptr;
+    static std::mutex mu;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!idx) {
+            idx = new std::map<std::string, const GB_builtin_entry *>();
+            for (const GB_builtin_entry *e = GB_builtin_registry; e->name; e++) (*idx)[e->name] = e;
+        }
+    }
+    auto it = idx->find(name);
+    if (it == idx->end()) return GrB_INVALID_VALUE;
+    *handle = it->second->obj;
+    *kind = it->second->kind;
+    return GrB_SUCCESS;
+}
+
+GrB_Info GxB_name(const char **name, const void *obj) {
+    if (!name || !obj) return GrB_NULL_POINTER;
+    // every builtin struct starts with magic; the name field position differs per kind
+    for (const GB_builtin_entry *e = GB_builtin_registry; e->name; e++) {
+        if (e->obj == obj) {
+            *name = e->name;
+            return GrB_SUCCESS;
+        }
+    }
+    return GrB_INVALID_VALUE;
+}
+
+// builtin types/ops are static: freeing is a no-op (as for SuiteSparse builtins)
+GrB_Info GrB_Type_free(GrB_Type *t) {
+    (void)t;
+    return GrB_SUCCESS;
+}
+GrB_Info GrB_BinaryOp_free(GrB_BinaryOp *op) {
+    (void)op;
+    return GrB_SUCCESS;
+}
+GrB_Info GrB_Monoid_free(GrB_Monoid *m) {
+    (void)m;
+    return GrB_SUCCESS;
+}
+GrB_Info GrB_Semiring_free(GrB_Semiring *s) {
+    (void)s;
+    return GrB_SUCCESS;
+}
+GrB_Info GxB_Semiring_add(GrB_Monoid *add, GrB_Semiring s) {
+    if (!add || !s) return GrB_NULL_POINTER;
+    *add = s->add;
+    return GrB_SUCCESS;
+}
+GrB_Info GxB_Semiring_multiply(GrB_BinaryOp *mul, GrB_Semiring s) {
+    if (!mul || !s) return GrB_NULL_POINTER;
+    *mul = s->mul;
+    return GrB_SUCCESS;
+}
+
+GrB_Info GrB_Descriptor_new(GrB_Descriptor *desc) {
+    if (!desc) return GrB_NULL_POINTER;
+    GB_Descriptor_opaque *d = new (std::nothrow) GB_Descriptor_opaque{GB_MAGIC, 0, 0, 0, 0, false, "desc"};
+    if (!d) return GrB_OUT_OF_MEMORY;
+    *desc = d;
+    return GrB_SUCCESS;
+}
+
+GrB_Info GrB_Descriptor_set(GrB_Descriptor d, GrB_Desc_Field field, GrB_Desc_Value val) {
+    if (!d) return GrB_NULL_POINTER;
+    if (d->magic != GB_MAGIC) return GrB_UNINITIALIZED_OBJECT;
+    if (d->builtin) return GrB_INVALID_VALUE;  // predefined descriptors are read-only
+    switch (field) {
+    case GrB_OUTP:
+        if (val != GxB_DEFAULT && val != GrB_REPLACE) return GrB_INVALID_VALUE;
+        d->outp = val;
+        break;
+    case GrB_MASK:
+        if (val == GxB_DEFAULT) d->mask = 0;
+        else if (val == GrB_COMP || val == GrB_STRUCTURE || val == GrB_COMP_STRUCTURE) d->mask |= val;
+        else return GrB_INVALID_VALUE;
+        break;
+    case GrB_INP0:
+        if (val != GxB_DEFAULT && val != GrB_TRAN) return GrB_INVALID_VALUE;
+        d->inp0 = val;
+        break;
+    case GrB_INP1:
+        if (val != GxB_DEFAULT && val != GrB_TRAN) return GrB_INVALID_VALUE;
+        d->inp1 = val;
+        break;
+    default: return GrB_INVALID_VALUE;
+    }
+    return GrB_SUCCESS;
+}
+
+GrB_Info GrB_Descriptor_free(GrB_Descriptor *desc) {
+    if (!desc) return GrB_NULL_POINTER;
+    if (*desc && !(*desc)->builtin) {
+        (*desc)->magic = GB_FREED;
+        delete *desc;
+    }
+    *desc = nullptr;
+    return GrB_SUCCESS;
+}
+
+}  // extern "C"

@@ -1,0 +1,372 @@
+// gb_device.cuh -- device-side value semantics for the GraphBLAS builtins.
+//
+// Typecasts, binary operators and monoids evaluated on gfx950.  The semantics
+// are the GraphBLAS C API 2.0 ones with SuiteSparse:GraphBLAS 7.4.x's builtin
+// definitions (integer ops wrap; x/0 saturates; float->int casts saturate and
+// map NaN to 0; bool PLUS/TIMES/MIN/MAX/MINUS are LOR/LAND/LAND/LOR/LXOR).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <type_traits>
+
+#include "../../include/gbamd_codes.h"
+
+#define GB_DEV __device__ __forceinline__
+#define GB_HD __host__ __device__ __forceinline__
+
+template <class T>
+struct gb_traits {
+    static constexpr bool is_bool = std::is_same<T, bool>::value;
+    static constexpr bool is_float = std::is_floating_point<T>::value;
+    static constexpr bool is_signed = std::is_signed<T>::value && !is_float;
+    static constexpr bool is_int = std::is_integral<T>::value && !is_bool;
+};
+
+template <class T>
+GB_HD T gb_tmax() {
+    if constexpr (std::is_same<T, bool>::value) return true;
+    else if constexpr (std::is_same<T, float>::value) return __builtin_inff();
+    else if constexpr (std::is_same<T, double>::value) return __builtin_inf();
+    else if constexpr (std::is_signed<T>::value) return (T)(~(typename std::make_unsigned<T>::type)0 >> 1);
+    else return (T)~(T)0;
+}
+template <class T>
+GB_HD T gb_tmin() {
+    if constexpr (std::is_same<T, bool>::value) return false;
+    else if constexpr (std::is_same<T, float>::value) return -__builtin_inff();
+    else if constexpr (std::is_same<T, double>::value) return -__builtin_inf();
+    else if constexpr (std::is_signed<T>::value) return (T)(-gb_tmax<T>() - 1);
+    else return (T)0;
+}
+
+// ------------------------------------------------------------------ casts
+template <class D, class S>
+GB_HD D gb_cast(S x) {
+    if constexpr (std::is_same<D, S>::value) {
+        return x;
+    } else if constexpr (std::is_same<D, bool>::value) {
+        return x != (S)0;
+    } else if constexpr (std::is_floating_point<S>::value && std::is_integral<D>::value) {
+        // SuiteSparse GB_cast_to_int*: NaN -> 0, saturate, else truncate
+        if (x != x) return (D)0;
+        if (x <= (S)gb_tmin<D>()) return gb_tmin<D>();
+        if (x >= (S)gb_tmax<D>()) return gb_tmax<D>();
+        return (D)x;
+    } else if constexpr (std::is_same<S, bool>::value) {
+        return (D)(x ? 1 : 0);
+    } else if constexpr (std::is_integral<S>::value && std::is_integral<D>::value) {
+        // two's complement wrap (modular)
+        using UD = typename std::make_unsigned<D>::type;
+        return (D)(UD)(typename std::make_unsigned<S>::type)x;
+    } else {
+        return (D)x;
+    }
+}
+
+// ------------------------------------------------------------------ ops
+GB_HD bool gb_op_is_positional(int op) { return op >= GBAMD_OP_FIRSTI; }
+GB_HD bool gb_op_is_cmp(int op) { return op >= GBAMD_OP_EQ && op <= GBAMD_OP_LE; }
+
+GB_HD int gb_bool_rename(int op) {
+    switch (op) {
+    case GBAMD_OP_PLUS: case GBAMD_OP_MAX: return GBAMD_OP_LOR;
+    case GBAMD_OP_TIMES: case GBAMD_OP_MIN: return GBAMD_OP_LAND;
+    case GBAMD_OP_MINUS: case GBAMD_OP_RMINUS: case GBAMD_OP_ISNE: case GBAMD_OP_NE: return GBAMD_OP_LXOR;
+    case GBAMD_OP_DIV: return GBAMD_OP_FIRST;
+    case GBAMD_OP_RDIV: return GBAMD_OP_SECOND;
+    case GBAMD_OP_ISEQ: case GBAMD_OP_EQ: return GBAMD_OP_LXNOR;
+    case GBAMD_OP_ISGT: return GBAMD_OP_GT;
+    case GBAMD_OP_ISLT: return GBAMD_OP_LT;
+    case GBAMD_OP_ISGE: return GBAMD_OP_GE;
+    case GBAMD_OP_ISLE: return GBAMD_OP_LE;
+    default: return op;
+    }
+}
+
+template <class T>
+GB_HD T gb_idiv(T x, T y) {
+    if constexpr (std::is_signed<T>::value) {
+        if (y == (T)-1) return (T)((typename std::make_unsigned<T>::type)0 - (typename std::make_unsigned<T>::type)x);
+        if (y == 0) return x == 0 ? (T)0 : (x < 0 ? gb_tmin<T>() : gb_tmax<T>());
+        return (T)(x / y);
+    } else {
+        if (y == 0) return x == 0 ? (T)0 : gb_tmax<T>();
+        return (T)(x / y);
+    }
+}
+
+template <class T>
+GB_HD bool gb_cmp(int op, T x, T y) {
+    switch (op) {
+    case GBAMD_OP_EQ: return x == y;
+    case GBAMD_OP_NE: return x != y;
+    case GBAMD_OP_GT: return x > y;
+    case GBAMD_OP_LT: return x < y;
+    case GBAMD_OP_GE: return x >= y;
+    case GBAMD_OP_LE: return x <= y;
+    default: return false;
+    }
+}
+
+template <class T>
+GB_HD T gb_wrap_add(T x, T y) {
+    if constexpr (gb_traits<T>::is_int) {
+        using U = typename std::make_unsigned<T>::type;
+        return (T)(U)((U)x + (U)y);
+    } else return x + y;
+}
+template <class T>
+GB_HD T gb_wrap_sub(T x, T y) {
+    if constexpr (gb_traits<T>::is_int) {
+        using U = typename std::make_unsigned<T>::type;
+        return (T)(U)((U)x - (U)y);
+    } else return x - y;
+}
+template <class T>
+GB_HD T gb_wrap_mul(T x, T y) {
+    if constexpr (gb_traits<T>::is_int) {
+        using U = typename std::make_unsigned<T>::type;
+        // promote narrow unsigned to 64-bit to avoid int promotion UB
+        return (T)(U)((uint64_t)(U)x * (uint64_t)(U)y);
+    } else return x * y;
+}
+template <class T>
+GB_HD T gb_min(T x, T y) {
+    if constexpr (std::is_floating_point<T>::value) return fmin(x, y);
+    else return x < y ? x : y;
+}
+template <class T>
+GB_HD T gb_max(T x, T y) {
+    if constexpr (std::is_floating_point<T>::value) return fmax(x, y);
+    else return x > y ? x : y;
+}
+
+// z = op(x, y), x, y, z all of type T (non-positional, non-comparison ops;
+// comparison ops return 1/0 of type T here, which callers cast).
+template <class T>
+GB_HD T gb_binop(int op, T x, T y) {
+    if constexpr (std::is_same<T, bool>::value) {
+        op = gb_bool_rename(op);
+        switch (op) {
+        case GBAMD_OP_FIRST: return x;
+        case GBAMD_OP_SECOND: case GBAMD_OP_ANY: return y;
+        case GBAMD_OP_PAIR: return true;
+        case GBAMD_OP_LOR: return x || y;
+        case GBAMD_OP_LAND: return x && y;
+        case GBAMD_OP_LXOR: return x != y;
+        case GBAMD_OP_LXNOR: return x == y;
+        case GBAMD_OP_GT: return x && !y;
+        case GBAMD_OP_LT: return !x && y;
+        case GBAMD_OP_GE: return x || !y;
+        case GBAMD_OP_LE: return !x || y;
+        case GBAMD_OP_POW: return x || !y;
+        case GBAMD_OP_BOR: return x || y;
+        case GBAMD_OP_BAND: return x && y;
+        case GBAMD_OP_BXOR: return x != y;
+        case GBAMD_OP_BXNOR: return x == y;
+        default: return false;
+        }
+    } else {
+        const T one = (T)1, zero = (T)0;
+        switch (op) {
+        case GBAMD_OP_FIRST: return x;
+        case GBAMD_OP_SECOND: case GBAMD_OP_ANY: return y;
+        case GBAMD_OP_PAIR: return one;
+        case GBAMD_OP_MIN: return gb_min(x, y);
+        case GBAMD_OP_MAX: return gb_max(x, y);
+        case GBAMD_OP_PLUS: return gb_wrap_add(x, y);
+        case GBAMD_OP_MINUS: return gb_wrap_sub(x, y);
+        case GBAMD_OP_RMINUS: return gb_wrap_sub(y, x);
+        case GBAMD_OP_TIMES: return gb_wrap_mul(x, y);
+        case GBAMD_OP_DIV:
+            if constexpr (gb_traits<T>::is_int) return gb_idiv(x, y);
+            else return x / y;
+        case GBAMD_OP_RDIV:
+            if constexpr (gb_traits<T>::is_int) return gb_idiv(y, x);
+            else return y / x;
+        case GBAMD_OP_POW:
+            if constexpr (std::is_same<T, float>::value) return powf(x, y);
+            else if constexpr (std::is_same<T, double>::value) return pow(x, y);
+            else return gb_cast<T, double>(pow((double)x, (double)y));
+        case GBAMD_OP_ISEQ: return x == y ? one : zero;
+        case GBAMD_OP_ISNE: return x != y ? one : zero;
+        case GBAMD_OP_ISGT: return x > y ? one : zero;
+        case GBAMD_OP_ISLT: return x < y ? one : zero;
+        case GBAMD_OP_ISGE: return x >= y ? one : zero;
+        case GBAMD_OP_ISLE: return x <= y ? one : zero;
+        case GBAMD_OP_LOR: return (x != zero || y != zero) ? one : zero;
+        case GBAMD_OP_LAND: return (x != zero && y != zero) ? one : zero;
+        case GBAMD_OP_LXOR: return ((x != zero) != (y != zero)) ? one : zero;
+        case GBAMD_OP_LXNOR: return ((x != zero) == (y != zero)) ? one : zero;
+        case GBAMD_OP_EQ: return x == y ? one : zero;
+        case GBAMD_OP_NE: return x != y ? one : zero;
+        case GBAMD_OP_GT: return x > y ? one : zero;
+        case GBAMD_OP_LT: return x < y ? one : zero;
+        case GBAMD_OP_GE: return x >= y ? one : zero;
+        case GBAMD_OP_LE: return x <= y ? one : zero;
+        default: break;
+        }
+        if constexpr (gb_traits<T>::is_int) {
+            using U = typename std::make_unsigned<T>::type;
+            switch (op) {
+            case GBAMD_OP_BOR: return (T)((U)x | (U)y);
+            case GBAMD_OP_BAND: return (T)((U)x & (U)y);
+            case GBAMD_OP_BXOR: return (T)((U)x ^ (U)y);
+            case GBAMD_OP_BXNOR: return (T)(U)~((U)x ^ (U)y);
+            default: break;
+            }
+        }
+        return zero;
+    }
+}
+
+GB_HD int64_t gb_posop(int op, int64_t i, int64_t k, int64_t j) {
+    switch (op) {
+    case GBAMD_OP_FIRSTI: return i;
+    case GBAMD_OP_FIRSTI1: return i + 1;
+    case GBAMD_OP_FIRSTJ: return k;
+    case GBAMD_OP_FIRSTJ1: return k + 1;
+    case GBAMD_OP_SECONDI: return k;
+    case GBAMD_OP_SECONDI1: return k + 1;
+    case GBAMD_OP_SECONDJ: return j;
+    case GBAMD_OP_SECONDJ1: return j + 1;
+    default: return 0;
+    }
+}
+
+// general binary op with output type Z (comparison ops produce bool)
+template <class X, class Z>
+GB_HD Z gb_binop_z(int op, X x, X y, int64_t i, int64_t k, int64_t j) {
+    if (gb_op_is_positional(op)) return gb_cast<Z, int64_t>(gb_posop(op, i, k, j));
+    if (gb_op_is_cmp(op)) {
+        if constexpr (std::is_same<X, bool>::value) return gb_cast<Z, bool>(gb_binop<bool>(op, x, y));
+        else return gb_cast<Z, bool>(gb_cmp<X>(op, x, y));
+    }
+    return gb_cast<Z, X>(gb_binop<X>(op, x, y));
+}
+
+// ------------------------------------------------------------------ monoids
+template <class T>
+GB_HD T gb_monoid(int m, T x, T y) {
+    switch (m) {
+    case GBAMD_MON_PLUS: return gb_binop<T>(GBAMD_OP_PLUS, x, y);
+    case GBAMD_MON_TIMES: return gb_binop<T>(GBAMD_OP_TIMES, x, y);
+    case GBAMD_MON_MIN: return gb_binop<T>(GBAMD_OP_MIN, x, y);
+    case GBAMD_MON_MAX: return gb_binop<T>(GBAMD_OP_MAX, x, y);
+    case GBAMD_MON_ANY: return x;
+    case GBAMD_MON_LOR: return gb_binop<T>(GBAMD_OP_LOR, x, y);
+    case GBAMD_MON_LAND: return gb_binop<T>(GBAMD_OP_LAND, x, y);
+    case GBAMD_MON_LXOR: return gb_binop<T>(GBAMD_OP_LXOR, x, y);
+    case GBAMD_MON_LXNOR: return gb_binop<T>(GBAMD_OP_LXNOR, x, y);
+    case GBAMD_MON_BOR: return gb_binop<T>(GBAMD_OP_BOR, x, y);
+    case GBAMD_MON_BAND: return gb_binop<T>(GBAMD_OP_BAND, x, y);
+    case GBAMD_MON_BXOR: return gb_binop<T>(GBAMD_OP_BXOR, x, y);
+    case GBAMD_MON_BXNOR: return gb_binop<T>(GBAMD_OP_BXNOR, x, y);
+    default: return x;
+    }
+}
+
+// terminal value of a monoid: once reached, further terms cannot change it
+template <class T>
+GB_HD bool gb_monoid_terminal(int m, T z) {
+    switch (m) {
+    case GBAMD_MON_ANY: return true;
+    case GBAMD_MON_LOR: return z != (T)0;
+    case GBAMD_MON_LAND: return z == (T)0;
+    case GBAMD_MON_MIN:
+        if constexpr (std::is_floating_point<T>::value) return false;  // NaN-ignoring fmin
+        else return z == gb_tmin<T>();
+    case GBAMD_MON_MAX:
+        if constexpr (std::is_floating_point<T>::value) return false;
+        else return z == gb_tmax<T>();
+    case GBAMD_MON_TIMES:
+        if constexpr (gb_traits<T>::is_int) return z == (T)0;
+        else return false;
+    case GBAMD_MON_BOR:
+        if constexpr (gb_traits<T>::is_int) return z == (T)~(T)0;
+        else return false;
+    case GBAMD_MON_BAND:
+        if constexpr (gb_traits<T>::is_int) return z == (T)0;
+        else return false;
+    default: return false;
+    }
+}
+
+// ------------------------------------------------------------------ semirings
+// Runtime-op semiring (generic path): every builtin (monoid, multiply) pair.
+template <class X, class Z>
+struct gb_sr_dyn {
+    int mon, mul;
+    GB_DEV Z mult(X a, X b, int64_t i, int64_t k, int64_t j) const {
+        return gb_binop_z<X, Z>(mul, a, b, i, k, j);
+    }
+    GB_DEV Z add(Z x, Z y) const { return gb_monoid<Z>(mon, x, y); }
+    GB_DEV bool terminal(Z z) const { return gb_monoid_terminal<Z>(mon, z); }
+    static constexpr bool reads_values = true;
+};
+
+// Compile-time semirings for the configured hot paths.
+template <class T>
+struct gb_sr_plus_times {
+    GB_DEV T mult(T a, T b, int64_t, int64_t, int64_t) const { return gb_wrap_mul(a, b); }
+    GB_DEV T add(T x, T y) const { return gb_wrap_add(x, y); }
+    GB_DEV bool terminal(T) const { return false; }
+    static constexpr bool reads_values = true;
+};
+template <class T>
+struct gb_sr_min_plus {
+    GB_DEV T mult(T a, T b, int64_t, int64_t, int64_t) const { return gb_wrap_add(a, b); }
+    GB_DEV T add(T x, T y) const { return gb_min(x, y); }
+    GB_DEV bool terminal(T z) const {
+        if constexpr (std::is_floating_point<T>::value) return false;
+        else return z == gb_tmin<T>();
+    }
+    static constexpr bool reads_values = true;
+};
+template <class T>
+struct gb_sr_any_pair {
+    GB_DEV T mult(T, T, int64_t, int64_t, int64_t) const { return (T)1; }
+    GB_DEV T add(T x, T) const { return x; }
+    GB_DEV bool terminal(T) const { return true; }
+    static constexpr bool reads_values = false;
+};
+struct gb_sr_lor_land {
+    GB_DEV bool mult(bool a, bool b, int64_t, int64_t, int64_t) const { return a && b; }
+    GB_DEV bool add(bool x, bool y) const { return x || y; }
+    GB_DEV bool terminal(bool z) const { return z; }
+    static constexpr bool reads_values = true;
+};
+
+// ------------------------------------------------------------------ wave helpers
+GB_DEV int gb_lane() { return __lane_id(); }
+
+template <class T>
+GB_DEV T gb_shfl_xor(T v, int mask, int width) {
+    if constexpr (sizeof(T) == 8) {
+        int64_t x;
+        __builtin_memcpy(&x, &v, 8);
+        int lo = __shfl_xor((int)(x & 0xffffffff), mask, width);
+        int hi = __shfl_xor((int)(x >> 32), mask, width);
+        int64_t y = ((int64_t)(uint32_t)lo) | ((int64_t)hi << 32);
+        T r;
+        __builtin_memcpy(&r, &y, 8);
+        return r;
+    } else if constexpr (sizeof(T) == 4) {
+        int x;
+        __builtin_memcpy(&x, &v, 4);
+        x = __shfl_xor(x, mask, width);
+        T r;
+        __builtin_memcpy(&r, &x, 4);
+        return r;
+    } else {
+        int x = 0;
+        __builtin_memcpy(&x, &v, sizeof(T));
+        x = __shfl_xor(x, mask, width);
+        T r;
+        __builtin_memcpy(&r, &x, sizeof(T));
+        return r;
+    }
+}
+
+GB_DEV bool gb_bit(const uint64_t *bits, int64_t i) { return (bits[i >> 6] >> (i & 63)) & 1ULL; }

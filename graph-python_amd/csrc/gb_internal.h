@@ -1,0 +1,288 @@
+// gb_internal.h -- object model and host-side helpers of libgraphblas_amd.so.
+//
+// One object struct backs GrB_Matrix, GrB_Vector and GrB_Scalar, so the pointer
+// casts python-graphblas performs ((GrB_Matrix)v in Vector.inner/outer,
+// reference core/vector.py:1643,1686; Vector._as_matrix core/vector.py:186-205;
+// Scalar._as_vector core/scalar.py:555-573) are legal: the operation looks at
+// the object's kind and converts storage on the fly.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "../../include/gbamd_codes.h"
+#include "../../include/graphblas_amd.h"
+
+#define GB_MAGIC 0x6d614d424731ULL   // live object
+#define GB_FREED 0x646565724642ULL   // freed object
+
+struct GB_Type_opaque {
+    uint64_t magic;
+    int code;
+    size_t size;
+    const char *name;
+};
+struct GB_BinaryOp_opaque {
+    uint64_t magic;
+    int opcode;
+    GrB_Type xtype, ytype, ztype;  // xtype == nullptr: positional op
+    const char *name;
+};
+struct GB_Monoid_opaque {
+    uint64_t magic;
+    int mcode;
+    GrB_Type type;
+    GrB_BinaryOp op;
+    const char *name;
+};
+struct GB_Semiring_opaque {
+    uint64_t magic;
+    GrB_Monoid add;
+    GrB_BinaryOp mul;
+    const char *name;
+};
+struct GB_Descriptor_opaque {
+    uint64_t magic;
+    int outp, mask, inp0, inp1;
+    bool builtin;
+    const char *name;
+};
+
+struct GB_builtin_entry {
+    const char *name;
+    int kind;
+    void *obj;
+};
+extern const GB_builtin_entry GB_builtin_registry[];
+
+enum { GB_KIND_MATRIX = 0, GB_KIND_VECTOR = 1, GB_KIND_SCALAR = 2 };
+
+// Device storage.  CSR for matrices; bitmap + dense values for vectors/scalars.
+struct GB_Matrix_opaque {
+    uint64_t magic;
+    int kind;
+    GrB_Type type;
+    int64_t nrows, ncols;
+    bool iso;            // values hold one element that applies to every entry
+    // ---- CSR (kind == MATRIX)
+    int64_t nvals;       // exact, host-known for CSR
+    int64_t *rowptr;     // [nrows+1]
+    int32_t *colidx;     // [nvals]
+    void *vals;          // [nvals] or [1] when iso
+    // cached transpose (CSC), built lazily by gb_csc()
+    bool t_valid;
+    int64_t *t_rowptr;
+    int32_t *t_colidx;
+    void *t_vals;
+    // ---- bitmap (kind == VECTOR / SCALAR); length n = nrows (ncols == 1)
+    uint64_t *bits;      // [ceil(n/64)]
+    void *dense;         // [n] or [1] when iso
+    int64_t *d_nvals;    // device counter kept current by every writer
+    bool nvals_valid;    // host copy in `nvals` is current
+    std::string err;
+};
+typedef GB_Matrix_opaque GB_Obj;
+
+inline GB_Obj *OBJ(const void *p) { return (GB_Obj *)p; }
+
+// ------------------------------------------------------------------ errors
+struct gb_exception {
+    GrB_Info info;
+    std::string msg;
+};
+[[noreturn]] void gb_throw(GrB_Info info, const std::string &msg);
+#define GB_REQUIRE(cond, info, msg) \
+    do {                            \
+        if (!(cond)) gb_throw(info, msg); \
+    } while (0)
+void gb_hip_check(hipError_t e, const char *what);
+#define GB_HIP(x) gb_hip_check((x), #x)
+#define GB_LAUNCH_CHECK() gb_hip_check(hipGetLastError(), "kernel launch")
+
+// API-boundary wrapper: runs body, converts exceptions to GrB_Info and stores
+// the message on the error object (reference core/exceptions.py:124-155 reads
+// it back with GrB_<Type>_error on the call's output argument).
+template <class F>
+GrB_Info gb_api(GB_Obj *errobj, F &&body) {
+    try {
+        body();
+        if (errobj && errobj->magic == GB_MAGIC) errobj->err.clear();
+        return GrB_SUCCESS;
+    } catch (const gb_exception &e) {
+        if (errobj && errobj->magic == GB_MAGIC) errobj->err = e.msg;
+        return e.info;
+    } catch (const std::bad_alloc &) {
+        if (errobj && errobj->magic == GB_MAGIC) errobj->err = "out of host memory";
+        return GrB_OUT_OF_MEMORY;
+    } catch (...) {
+        return GrB_PANIC;
+    }
+}
+
+// ------------------------------------------------------------------ context
+hipStream_t gb_stream();
+void gb_require_init();
+void gb_sync();
+int64_t gb_knob(const char *key);  // tuning knobs (0 = auto)
+
+// device memory (stream-ordered pool on the library stream)
+void *gb_malloc(size_t bytes);        // throws GrB_OUT_OF_MEMORY
+void gb_free(void *p);
+template <class T>
+T *gb_malloc_n(size_t n) {
+    return (T *)gb_malloc(n * sizeof(T));
+}
+void gb_memset(void *p, int v, size_t bytes);
+void gb_copy_d2d(void *dst, const void *src, size_t bytes);
+void gb_copy_h2d(void *dst, const void *src, size_t bytes);
+void gb_copy_d2h(void *dst, const void *src, size_t bytes);  // synchronises
+
+// scratch owner: frees device buffers at scope exit (stream ordered)
+struct gb_scratch {
+    void *ptrs[32];
+    int n = 0;
+    template <class T>
+    T *get(size_t count) {
+        T *p = gb_malloc_n<T>(count ? count : 1);
+        ptrs[n++] = p;
+        return p;
+    }
+    ~gb_scratch() {
+        for (int i = 0; i < n; i++) gb_free(ptrs[i]);
+    }
+};
+
+// ------------------------------------------------------------------ objects
+GB_Obj *gb_obj_check(const void *p, bool allow_null = false);
+GB_Obj *gb_new_object(int kind, GrB_Type type, int64_t nrows, int64_t ncols);
+void gb_obj_free_storage(GB_Obj *A);
+void gb_drop_transpose(GB_Obj *A);
+int64_t gb_nvals(GB_Obj *A);           // exact (may synchronise for bitmaps)
+inline int64_t gb_words(int64_t n) { return (n + 63) >> 6; }
+inline bool gb_is_bitmap(const GB_Obj *A) { return A->kind != GB_KIND_MATRIX; }
+
+// Typecast a device array (n elements, or the single iso value).
+void gb_cast_array(void *dst, int dst_code, const void *src, int src_code, int64_t n);
+
+// Read-only CSR view of any object (a vector becomes an n x 1 CSR temporary).
+struct gb_csr_view {
+    int64_t nrows = 0, ncols = 0, nvals = 0;
+    const int64_t *rowptr = nullptr;
+    const int32_t *colidx = nullptr;
+    const void *vals = nullptr;
+    bool iso = false;
+    int tcode = 0;
+    gb_scratch own;
+};
+void gb_get_csr(gb_csr_view &v, GB_Obj *A);
+// CSC of A (i.e. CSR of A^T), cached on the object when A is a matrix.
+void gb_get_csc(gb_csr_view &v, GB_Obj *A);
+// Values of a CSR view cast to type `code` (returns the view's own pointer if same type).
+const void *gb_view_vals_as(gb_csr_view &v, int code, gb_scratch &s);
+
+// Read-only bitmap view of any object (an n x 1 matrix becomes a bitmap temporary).
+struct gb_bitmap_view {
+    int64_t n = 0;
+    const uint64_t *bits = nullptr;
+    const void *vals = nullptr;
+    bool iso = false;
+    int tcode = 0;
+    gb_scratch own;
+};
+void gb_get_bitmap(gb_bitmap_view &v, GB_Obj *A);
+const void *gb_bitmap_vals_as(gb_bitmap_view &v, int code, gb_scratch &s);
+
+// Install freshly computed storage into an object (takes ownership).
+void gb_install_csr(GB_Obj *C, int64_t nrows, int64_t ncols, int64_t nvals, int64_t *rowptr,
+                    int32_t *colidx, void *vals, bool iso);
+void gb_install_bitmap(GB_Obj *C, int64_t n, uint64_t *bits, void *dense, bool iso,
+                       int64_t *d_nvals /* may be null: recomputed */);
+
+// bitmap helpers (device work on the library stream)
+void gb_bitmap_count(const uint64_t *bits, int64_t n, int64_t *d_count);
+void gb_bitmap_to_csr(const uint64_t *bits, const void *dense, bool iso, int64_t n, size_t tsize,
+                      int64_t **rowptr, int32_t **colidx, void **vals, int64_t *nvals);
+void gb_csr_col_to_bitmap(const gb_csr_view &v, size_t tsize, uint64_t **bits, void **dense,
+                          int64_t **d_nvals);
+
+// COO build (sort + duplicate fold) into an empty object; extract tuples to host
+void gb_build(GB_Obj *C, const GrB_Index *I, const GrB_Index *J, const void *X, int xcode, bool x_iso,
+              int64_t n, GrB_BinaryOp dup);
+void gb_extract_tuples(GB_Obj *A, GrB_Index *I, GrB_Index *J, void *X, int xcode, GrB_Index *nvals);
+
+// expand iso values to a full array of n elements
+void *gb_expand_iso(const void *one_value, size_t tsize, int64_t n);
+
+// transpose CSR -> CSR of the transpose (values optional)
+void gb_transpose_csr(int64_t nrows, int64_t ncols, int64_t nvals, const int64_t *rowptr,
+                      const int32_t *colidx, const void *vals, size_t tsize, bool iso,
+                      int64_t **trowptr, int32_t **tcolidx, void **tvals);
+
+// ------------------------------------------------------------------ ops
+struct gb_desc {
+    bool replace = false, comp = false, structure = false, tran0 = false, tran1 = false;
+};
+gb_desc gb_read_desc(const GrB_Descriptor d);
+
+// Effective mask: bitmap of positions where the mask is true (value masks cast
+// to bool), for vector outputs; CSR (structure only) for matrix outputs.
+struct gb_vmask {
+    const uint64_t *bits = nullptr;  // nullptr: no mask
+    bool comp = false;
+    gb_scratch own;
+};
+void gb_make_vmask(gb_vmask &m, GB_Obj *M, const gb_desc &d, int64_t n);
+
+struct gb_mmask {
+    bool present = false, comp = false;
+    gb_csr_view view;        // structure of the mask
+    const int64_t *rowptr = nullptr;
+    const int32_t *colidx = nullptr;
+    int64_t nvals = 0;
+    gb_scratch own;
+};
+void gb_make_mmask(gb_mmask &m, GB_Obj *M, const gb_desc &d, int64_t nrows, int64_t ncols);
+
+// Result of a computation before the write-back into C.
+struct gb_vec_result {  // bitmap, type code ztype
+    int64_t n = 0;
+    uint64_t *bits = nullptr;
+    void *dense = nullptr;
+    bool iso = false;
+    int tcode = 0;
+    int64_t *d_nvals = nullptr;
+};
+struct gb_mat_result {  // CSR
+    int64_t nrows = 0, ncols = 0, nvals = 0;
+    int64_t *rowptr = nullptr;
+    int32_t *colidx = nullptr;
+    void *vals = nullptr;
+    bool iso = false;
+    int tcode = 0;
+    bool within_mask = false;  // T already restricted to the (non-complemented) mask
+};
+
+// C<M,replace> = C accum T  (takes ownership of T's buffers)
+void gb_writeback_vector(GB_Obj *C, gb_vec_result &T, GB_Obj *M, const gb_desc &d,
+                         GrB_BinaryOp accum, bool t_within_mask);
+void gb_writeback_matrix(GB_Obj *C, gb_mat_result &T, GB_Obj *M, const gb_desc &d,
+                         GrB_BinaryOp accum);
+
+// kernels of the hot path (gb_mxv.hip, gb_mxm.hip)
+void gb_spmv(gb_vec_result &T, const gb_csr_view &A, gb_bitmap_view &u, const gb_vmask &mask,
+             GrB_Semiring sr, bool flip);
+void gb_spgemm(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, gb_csr_view *BT,
+               gb_mmask &mask, GrB_Semiring sr);
+
+// scans / sorts (gb_prim.hip)
+void gb_exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n);  // out[n] = total
+void gb_sort_pairs_u64(uint64_t *keys, int64_t *vals, int64_t n, int end_bit);
+void gb_sort_pairs_i32(int32_t *keys, int64_t *vals, int64_t n, int end_bit);
+int64_t gb_read_i64(const int64_t *dptr);
+
+const char *gb_type_name(int code);
+size_t gb_type_size(int code);
+GrB_Type gb_type_of(int code);

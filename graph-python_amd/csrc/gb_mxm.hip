@@ -1,0 +1,362 @@
+// gb_mxm.hip -- SpGEMM over a semiring: the kernels behind GrB_mxm
+// (replaces SuiteSparse's GB_AxB_dot3 / saxpy3 reached from reference
+// core/matrix.py:2241 and core/vector.py:1686).
+//
+// Two methods, chosen per call:
+//  * masked dot product (mask present, not complemented): T(i,j) is computed
+//    only for (i,j) in M, by merging row i of A' with row j of B'^T (the
+//    cached CSC).  Each entry folds its terms in ascending k.
+//  * Gustavson as expand-sort-compress (no mask / complemented mask): every
+//    product A'(i,k) B'(k,j) is written at a position ordered by (i, k, j),
+//    a stable radix sort on (i, j) groups the terms of each output entry
+//    without disturbing their k order, and one pass folds each run.  Rows are
+//    processed in chunks so the expanded products stay within a memory budget.
+// Both fold every output entry in ascending k, so floating-point results do
+// not depend on scheduling.
+#include <algorithm>
+#include <vector>
+
+#include "gb_dispatch.cuh"
+#include "gb_internal.h"
+
+#define MXM_BLOCK 256
+static inline unsigned mxm_grid(int64_t n, unsigned cap = 16384) {
+    int64_t g = (n + MXM_BLOCK - 1) / MXM_BLOCK;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+#define MXM_STRIDE(i, n) \
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (n); i += (int64_t)gridDim.x * blockDim.x)
+
+__global__ void k_rowof(const int64_t *__restrict__ rowptr, int64_t r0, int64_t r1, int64_t pbase,
+                        int64_t *__restrict__ rowof) {
+    int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    int lane = threadIdx.x & 63;
+    int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t i = r0 + wave; i < r1; i += nw)
+        for (int64_t p = rowptr[i] + lane; p < rowptr[i + 1]; p += 64) rowof[p - pbase] = i;
+}
+
+// ================================================================== masked dot
+template <class SR, class X, class Z>
+__global__ __launch_bounds__(MXM_BLOCK) void k_dot_masked(
+    SR sr, int64_t nm, const int64_t *__restrict__ mrowof, const int32_t *__restrict__ mci,
+    const int64_t *__restrict__ arp, const int32_t *__restrict__ aci, const X *__restrict__ avx, bool a_iso,
+    const int64_t *__restrict__ brp, const int32_t *__restrict__ bci, const X *__restrict__ bvx, bool b_iso,
+    Z *__restrict__ tval, int64_t *__restrict__ tflag) {
+    MXM_STRIDE(q, nm) {
+        const int64_t i = mrowof[q];
+        const int32_t j = mci[q];
+        int64_t pa = arp[i], ea = arp[i + 1], pb = brp[j], eb = brp[j + 1];
+        bool found = false;
+        Z acc = Z();
+        while (pa < ea && pb < eb) {
+            int32_t ka = aci[pa], kb = bci[pb];
+            if (ka < kb) {
+                // gallop in A when it is far behind
+                pa++;
+            } else if (kb < ka) {
+                pb++;
+            } else {
+                X a = X(), b = X();
+                if (SR::reads_values) {
+                    a = avx[a_iso ? 0 : pa];
+                    b = bvx[b_iso ? 0 : pb];
+                }
+                Z z = sr.mult(a, b, i, ka, j);
+                acc = found ? sr.add(acc, z) : z;
+                found = true;
+                if (sr.terminal(acc)) break;
+                pa++;
+                pb++;
+            }
+        }
+        tflag[q] = found ? 1 : 0;
+        if (found) tval[q] = acc;
+    }
+}
+
+__global__ void k_gather_rowptr(const int64_t *__restrict__ mrp, const int64_t *__restrict__ pos, int64_t nrows,
+                                int64_t *__restrict__ trp) {
+    MXM_STRIDE(i, nrows + 1) trp[i] = pos[mrp[i]];
+}
+
+template <class Z>
+__global__ void k_compact_dot(int64_t nm, const int64_t *__restrict__ flag, const int64_t *__restrict__ pos,
+                              const int32_t *__restrict__ mci, const Z *__restrict__ tval, int32_t *__restrict__ oci,
+                              Z *__restrict__ ovx) {
+    MXM_STRIDE(q, nm) {
+        if (flag[q]) {
+            int64_t o = pos[q];
+            oci[o] = mci[q];
+            if (ovx) ovx[o] = tval[q];
+        }
+    }
+}
+
+// ================================================================== Gustavson (ESC)
+__global__ void k_row_flops(const int64_t *__restrict__ arp, const int32_t *__restrict__ aci, int64_t nrows,
+                            const int64_t *__restrict__ brp, int64_t *__restrict__ fl) {
+    int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    int lane = threadIdx.x & 63;
+    int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t i = wave; i < nrows; i += nw) {
+        int64_t s = 0;
+        for (int64_t p = arp[i] + lane; p < arp[i + 1]; p += 64) {
+            int32_t k = aci[p];
+            s += brp[k + 1] - brp[k];
+        }
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+        if (lane == 0) fl[i] = s;
+    }
+}
+
+__global__ void k_entry_counts(const int32_t *__restrict__ aci, int64_t p0, int64_t np, const int64_t *__restrict__ brp,
+                               int64_t *__restrict__ cnt) {
+    MXM_STRIDE(q, np) {
+        int32_t k = aci[p0 + q];
+        cnt[q] = brp[k + 1] - brp[k];
+    }
+}
+
+// one wave per A' entry: the B' row is streamed by 64 lanes (coalesced)
+template <class SR, class X, class Z>
+__global__ __launch_bounds__(MXM_BLOCK) void k_expand(
+    SR sr, int64_t p0, int64_t np, int64_t r0, const int64_t *__restrict__ rowof, const int32_t *__restrict__ aci,
+    const X *__restrict__ avx, bool a_iso, const int64_t *__restrict__ brp, const int32_t *__restrict__ bci,
+    const X *__restrict__ bvx, bool b_iso, const int64_t *__restrict__ eoff, uint64_t *__restrict__ keys,
+    int64_t *__restrict__ perm, Z *__restrict__ vals) {
+    int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    int lane = threadIdx.x & 63;
+    int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t q = wave; q < np; q += nw) {
+        int64_t p = p0 + q;
+        int64_t i = rowof[q];
+        int32_t k = aci[p];
+        X a = X();
+        if (SR::reads_values) a = avx[a_iso ? 0 : p];
+        int64_t base = eoff[q], b0 = brp[k], b1 = brp[k + 1];
+        for (int64_t pb = b0 + lane; pb < b1; pb += 64) {
+            int32_t j = bci[pb];
+            X b = X();
+            if (SR::reads_values) b = bvx[b_iso ? 0 : pb];
+            int64_t o = base + (pb - b0);
+            keys[o] = ((uint64_t)(i - r0) << 32) | (uint32_t)j;
+            perm[o] = o;
+            if (vals) vals[o] = sr.mult(a, b, i, k, j);
+        }
+    }
+}
+
+__global__ void k_run_heads(const uint64_t *__restrict__ keys, int64_t n, int64_t *__restrict__ head) {
+    MXM_STRIDE(q, n) head[q] = (q == 0 || keys[q] != keys[q - 1]) ? 1 : 0;
+}
+
+template <class SR, class Z>
+__global__ void k_fold(SR sr, const uint64_t *__restrict__ keys, const int64_t *__restrict__ perm,
+                       const int64_t *__restrict__ pos, int64_t n, const Z *__restrict__ vals, int64_t r0,
+                       unsigned long long *__restrict__ rowcnt, int32_t *__restrict__ oci, Z *__restrict__ ovx) {
+    MXM_STRIDE(q, n) {
+        if (q != 0 && keys[q] == keys[q - 1]) continue;
+        int64_t o = pos[q];
+        oci[o] = (int32_t)(keys[q] & 0xffffffffULL);
+        atomicAdd(&rowcnt[r0 + (int64_t)(keys[q] >> 32)], 1ULL);
+        if (ovx) {
+            Z acc = vals[perm[q]];
+            for (int64_t r = q + 1; r < n && keys[r] == keys[q]; r++) {
+                if (sr.terminal(acc)) break;
+                acc = sr.add(acc, vals[perm[r]]);
+            }
+            ovx[o] = acc;
+        }
+    }
+}
+
+static bool idempotent(int m) {
+    return m == GBAMD_MON_ANY || m == GBAMD_MON_MIN || m == GBAMD_MON_MAX || m == GBAMD_MON_LOR ||
+           m == GBAMD_MON_LAND || m == GBAMD_MON_BOR || m == GBAMD_MON_BAND;
+}
+
+template <class SR, class X, class Z>
+__global__ void k_iso_value2(SR sr, const X *avals, const X *bvals, Z *out) {
+    X a = avals ? avals[0] : X(), b = bvals ? bvals[0] : X();
+    *out = sr.mult(a, b, 0, 0, 0);
+}
+
+void gb_spgemm(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, gb_csr_view *BT, gb_mmask &mask,
+               GrB_Semiring sr) {
+    gb_sr_info info = gb_sr_describe(sr);
+    gb_scratch s;
+    const void *av = info.reads_values ? gb_view_vals_as(A, info.xcode, s) : nullptr;
+    const int64_t nrows = A.nrows, ncols = B.ncols;
+    const size_t zs = gb_type_size(info.zcode);
+    bool reads_a = info.reads_values, reads_b = info.reads_values;
+    if (info.mul == GBAMD_OP_FIRST) reads_b = false;
+    if (info.mul == GBAMD_OP_SECOND) reads_a = false;
+    bool iso = !info.positional && idempotent(info.mon) && (!reads_a || A.iso) && (!reads_b || B.iso);
+    if (info.mul == GBAMD_OP_PAIR) iso = idempotent(info.mon);
+    T.nrows = nrows;
+    T.ncols = ncols;
+    T.tcode = info.zcode;
+    T.iso = iso;
+
+    const bool use_dot = mask.present && !mask.comp && BT != nullptr;
+    if (use_dot) {
+        const void *btv = info.reads_values ? gb_view_vals_as(*BT, info.xcode, s) : nullptr;
+        const int64_t nm = mask.nvals;
+        int64_t *mrowof = s.get<int64_t>(nm);
+        if (nm)
+            hipLaunchKernelGGL(k_rowof, dim3(mxm_grid(std::min<int64_t>(nrows * 64, 1LL << 22))), dim3(MXM_BLOCK), 0,
+                               gb_stream(), mask.rowptr, (int64_t)0, nrows, (int64_t)0, mrowof);
+        int64_t *flag = s.get<int64_t>(nm);
+        int64_t *pos = s.get<int64_t>(nm + 1);
+        void *tval = s.get<char>(nm * zs);
+        gb_dispatch_sr(info, [&](auto srf, auto x, auto z) {
+            using SRT = decltype(srf);
+            using X = decltype(x);
+            using Z = decltype(z);
+            if (nm)
+                hipLaunchKernelGGL((k_dot_masked<SRT, X, Z>), dim3(mxm_grid(nm)), dim3(MXM_BLOCK), 0, gb_stream(),
+                                   srf, nm, mrowof, mask.colidx, A.rowptr, A.colidx, (const X *)av, A.iso,
+                                   BT->rowptr, BT->colidx, (const X *)btv, BT->iso, (Z *)tval, flag);
+            GB_LAUNCH_CHECK();
+            gb_exclusive_scan_i64(flag, pos, nm);
+            int64_t nz = gb_read_i64(pos + nm);
+            T.rowptr = gb_malloc_n<int64_t>(nrows + 1);
+            hipLaunchKernelGGL(k_gather_rowptr, dim3(mxm_grid(nrows + 1)), dim3(MXM_BLOCK), 0, gb_stream(),
+                               mask.rowptr, pos, nrows, T.rowptr);
+            T.colidx = gb_malloc_n<int32_t>(nz);
+            T.vals = gb_malloc((iso ? 1 : nz) * zs);
+            if (nm)
+                hipLaunchKernelGGL(k_compact_dot<Z>, dim3(mxm_grid(nm)), dim3(MXM_BLOCK), 0, gb_stream(), nm, flag,
+                                   pos, mask.colidx, (const Z *)tval, T.colidx, iso ? nullptr : (Z *)T.vals);
+            if (iso)
+                hipLaunchKernelGGL((k_iso_value2<SRT, X, Z>), dim3(1), dim3(1), 0, gb_stream(), srf, (const X *)av,
+                                   (const X *)btv, (Z *)T.vals);
+            GB_LAUNCH_CHECK();
+            T.nvals = nz;
+        });
+        T.within_mask = true;
+        return;
+    }
+
+    // ---------------- Gustavson, expand-sort-compress in row chunks
+    const void *bv = info.reads_values ? gb_view_vals_as(B, info.xcode, s) : nullptr;
+    int64_t *fl = s.get<int64_t>(nrows + 1);
+    int64_t *flp = s.get<int64_t>(nrows + 1);
+    if (nrows)
+        hipLaunchKernelGGL(k_row_flops, dim3(mxm_grid(std::min<int64_t>(nrows * 64, 1LL << 22))), dim3(MXM_BLOCK), 0,
+                           gb_stream(), A.rowptr, A.colidx, nrows, B.rowptr, fl);
+    GB_LAUNCH_CHECK();
+    gb_exclusive_scan_i64(fl, flp, nrows);
+    const int64_t F = gb_read_i64(flp + nrows);
+    int64_t budget = gb_knob("esc_budget");
+    if (budget <= 0) budget = 1LL << 27;
+    // chunk boundaries (host)
+    std::vector<int64_t> bounds;
+    bounds.push_back(0);
+    if (F > budget) {
+        std::vector<int64_t> hp(nrows + 1);
+        gb_copy_d2h(hp.data(), flp, (nrows + 1) * sizeof(int64_t));
+        int64_t r = 0;
+        while (r < nrows) {
+            int64_t lim = hp[r] + budget;
+            int64_t e = std::upper_bound(hp.begin() + r + 1, hp.end(), lim) - hp.begin() - 1;
+            if (e <= r) e = r + 1;  // a single row larger than the budget
+            if (e > nrows) e = nrows;
+            bounds.push_back(e);
+            r = e;
+        }
+    } else {
+        bounds.push_back(nrows);
+    }
+    // row pointers of A' (host copy of the chunk boundaries' entry offsets)
+    std::vector<int64_t> chunk_nz;
+    std::vector<int32_t *> chunk_ci;
+    std::vector<void *> chunk_vx;
+    unsigned long long *rowcnt = s.get<unsigned long long>(nrows + 1);
+    gb_memset(rowcnt, 0, (nrows + 1) * sizeof(unsigned long long));
+    gb_dispatch_sr(info, [&](auto srf, auto x, auto z) {
+        using SRT = decltype(srf);
+        using X = decltype(x);
+        using Z = decltype(z);
+        for (size_t c = 0; c + 1 < bounds.size(); c++) {
+            const int64_t r0 = bounds[c], r1 = bounds[c + 1];
+            int64_t pr[2];
+            gb_copy_d2h(&pr[0], A.rowptr + r0, sizeof(int64_t));
+            gb_copy_d2h(&pr[1], A.rowptr + r1, sizeof(int64_t));
+            const int64_t p0 = pr[0], np = pr[1] - pr[0];
+            gb_scratch cs;
+            int64_t *cnt = cs.get<int64_t>(np + 1);
+            int64_t *eoff = cs.get<int64_t>(np + 1);
+            int64_t *rowof = cs.get<int64_t>(np);
+            if (np) {
+                hipLaunchKernelGGL(k_entry_counts, dim3(mxm_grid(np)), dim3(MXM_BLOCK), 0, gb_stream(), A.colidx, p0,
+                                   np, B.rowptr, cnt);
+                hipLaunchKernelGGL(k_rowof, dim3(mxm_grid(std::min<int64_t>((r1 - r0) * 64, 1LL << 22))),
+                                   dim3(MXM_BLOCK), 0, gb_stream(), A.rowptr, r0, r1, p0, rowof);
+                GB_LAUNCH_CHECK();
+            }
+            gb_exclusive_scan_i64(cnt, eoff, np);
+            const int64_t fc = gb_read_i64(eoff + np);
+            if (fc == 0) {
+                chunk_nz.push_back(0);
+                chunk_ci.push_back(nullptr);
+                chunk_vx.push_back(nullptr);
+                continue;
+            }
+            uint64_t *keys = cs.get<uint64_t>(fc);
+            int64_t *perm = cs.get<int64_t>(fc);
+            Z *vals = iso ? nullptr : cs.get<Z>(fc);
+            hipLaunchKernelGGL((k_expand<SRT, X, Z>), dim3(mxm_grid(std::min<int64_t>(np * 64, 1LL << 24))),
+                               dim3(MXM_BLOCK), 0, gb_stream(), srf, p0, np, r0, rowof, A.colidx, (const X *)av, A.iso,
+                               B.rowptr, B.colidx, (const X *)bv, B.iso, eoff, keys, perm, vals);
+            GB_LAUNCH_CHECK();
+            int rbits = 1;
+            while (rbits < 31 && (1LL << rbits) < (r1 - r0)) rbits++;
+            gb_sort_pairs_u64(keys, perm, fc, 32 + rbits);
+            int64_t *head = cs.get<int64_t>(fc);
+            int64_t *pos = cs.get<int64_t>(fc + 1);
+            hipLaunchKernelGGL(k_run_heads, dim3(mxm_grid(fc)), dim3(MXM_BLOCK), 0, gb_stream(), keys, fc, head);
+            GB_LAUNCH_CHECK();
+            gb_exclusive_scan_i64(head, pos, fc);
+            const int64_t nu = gb_read_i64(pos + fc);
+            int32_t *oci = gb_malloc_n<int32_t>(nu);
+            Z *ovx = iso ? nullptr : gb_malloc_n<Z>(nu);
+            hipLaunchKernelGGL((k_fold<SRT, Z>), dim3(mxm_grid(fc)), dim3(MXM_BLOCK), 0, gb_stream(), srf, keys, perm,
+                               pos, fc, (const Z *)vals, r0, rowcnt, oci, ovx);
+            GB_LAUNCH_CHECK();
+            chunk_nz.push_back(nu);
+            chunk_ci.push_back(oci);
+            chunk_vx.push_back(ovx);
+        }
+        int64_t nz = 0;
+        for (int64_t c : chunk_nz) nz += c;
+        T.rowptr = gb_malloc_n<int64_t>(nrows + 1);
+        gb_exclusive_scan_i64((const int64_t *)rowcnt, T.rowptr, nrows);
+        if (chunk_nz.size() == 1) {
+            T.colidx = chunk_ci[0] ? chunk_ci[0] : gb_malloc_n<int32_t>(1);
+            T.vals = iso ? gb_malloc(zs) : (chunk_vx[0] ? chunk_vx[0] : gb_malloc(zs));
+        } else {
+            T.colidx = gb_malloc_n<int32_t>(nz);
+            T.vals = gb_malloc((iso ? 1 : nz) * zs);
+            int64_t off = 0;
+            for (size_t c = 0; c < chunk_nz.size(); c++) {
+                if (chunk_nz[c]) {
+                    gb_copy_d2d(T.colidx + off, chunk_ci[c], chunk_nz[c] * sizeof(int32_t));
+                    if (!iso) gb_copy_d2d((char *)T.vals + off * zs, chunk_vx[c], chunk_nz[c] * zs);
+                }
+                off += chunk_nz[c];
+                gb_free(chunk_ci[c]);
+                gb_free(chunk_vx[c]);
+            }
+        }
+        if (iso)
+            hipLaunchKernelGGL((k_iso_value2<SRT, X, Z>), dim3(1), dim3(1), 0, gb_stream(), srf, (const X *)av,
+                               (const X *)bv, (Z *)T.vals);
+        GB_LAUNCH_CHECK();
+        T.nvals = nz;
+    });
+    T.within_mask = false;
+}

@@ -1,0 +1,720 @@
+// gb_ops.hip -- the GraphBLAS operations exported by the C ABI:
+//   GrB_mxm / GrB_mxv / GrB_vxm                      (the hot path)
+//   eWiseMult / eWiseAdd, assign, reduce, transpose  (loop companions used by
+//   python-graphblas's isequal (reference core/matrix.py:391-398) and the
+//   BFS/SSSP notebook loops)
+// Each call: validate -> views of the inputs (casting values to the operator's
+// input type) -> compute T on the device -> C<M,replace> = C accum T.
+#include <algorithm>
+#include <vector>
+
+#include "gb_dispatch.cuh"
+#include "gb_internal.h"
+
+#define OPS_BLOCK 256
+static inline unsigned ops_grid(int64_t n, unsigned cap = 16384) {
+    int64_t g = (n + OPS_BLOCK - 1) / OPS_BLOCK;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+#define OPS_STRIDE(i, n) \
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (n); i += (int64_t)gridDim.x * blockDim.x)
+
+static void check_semiring(GrB_Semiring sr) {
+    GB_REQUIRE(sr, GrB_NULL_POINTER, "semiring is NULL");
+    GB_REQUIRE(sr->magic == GB_MAGIC, GrB_UNINITIALIZED_OBJECT, "invalid semiring");
+}
+static void check_binop(GrB_BinaryOp op, bool allow_null) {
+    if (!op) {
+        GB_REQUIRE(allow_null, GrB_NULL_POINTER, "operator is NULL");
+        return;
+    }
+    GB_REQUIRE(op->magic == GB_MAGIC, GrB_UNINITIALIZED_OBJECT, "invalid operator");
+}
+static int64_t ncols_of(GB_Obj *A) { return A->kind == GB_KIND_MATRIX ? A->ncols : 1; }
+
+// ================================================================== mxv / vxm
+static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr, GB_Obj *A, GB_Obj *u,
+                    const gb_desc &d, bool vxm) {
+    check_semiring(sr);
+    check_binop(accum, true);
+    // rows of the operand matrix the kernel pulls along:
+    //   mxv:  w = A' u    -> rows of A'          (A' = A: CSR, A' = A^T: CSC)
+    //   vxm:  w = u' A'   -> rows of A'^T        (A' = A: CSC, A' = A^T: CSR)
+    bool use_csc = vxm ? !d.tran1 : d.tran0;
+    int64_t a_rows = (vxm ? (d.tran1 ? A->nrows : ncols_of(A)) : (d.tran0 ? ncols_of(A) : A->nrows));
+    int64_t a_cols = (vxm ? (d.tran1 ? ncols_of(A) : A->nrows) : (d.tran0 ? A->nrows : ncols_of(A)));
+    GB_REQUIRE(u->nrows == a_cols && ncols_of(u) == 1, GrB_DIMENSION_MISMATCH, "u size does not match A");
+    GB_REQUIRE(w->nrows == a_rows && ncols_of(w) == 1, GrB_DIMENSION_MISMATCH, "w size does not match A");
+    gb_csr_view av;
+    if (use_csc) gb_get_csc(av, A);
+    else gb_get_csr(av, A);
+    gb_bitmap_view uv;
+    gb_get_bitmap(uv, u);
+    gb_vmask m;
+    gb_make_vmask(m, mask, d, a_rows);
+    gb_vec_result T;
+    gb_spmv(T, av, uv, m, sr, vxm);
+    gb_writeback_vector(w, T, mask, d, accum, true);
+}
+
+// ================================================================== mxm
+static void do_mxm(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, GrB_Semiring sr, GB_Obj *A, GB_Obj *B,
+                   const gb_desc &d) {
+    check_semiring(sr);
+    check_binop(accum, true);
+    int64_t ar = d.tran0 ? ncols_of(A) : A->nrows, ac = d.tran0 ? A->nrows : ncols_of(A);
+    int64_t br = d.tran1 ? ncols_of(B) : B->nrows, bc = d.tran1 ? B->nrows : ncols_of(B);
+    GB_REQUIRE(ac == br, GrB_DIMENSION_MISMATCH, "inner dimensions of A and B do not match");
+    GB_REQUIRE(C->nrows == ar && ncols_of(C) == bc, GrB_DIMENSION_MISMATCH, "C dimensions do not match A*B");
+    gb_csr_view av, bv, btv;
+    if (d.tran0) gb_get_csc(av, A);
+    else gb_get_csr(av, A);
+    if (d.tran1) gb_get_csc(bv, B);
+    else gb_get_csr(bv, B);
+    gb_mmask m;
+    gb_make_mmask(m, M, d, ar, bc);
+    gb_csr_view *btp = nullptr;
+    int64_t method = gb_knob("mxm_method");  // 0 auto, 1 dot, 2 gustavson
+    if (m.present && !m.comp && method != 2) {
+        // B'^T: rows are the columns of B'
+        if (d.tran1) gb_get_csr(btv, B);
+        else gb_get_csc(btv, B);
+        btp = &btv;
+    }
+    gb_mat_result T;
+    gb_spgemm(T, av, bv, btp, m, sr);
+    gb_writeback_matrix(C, T, M, d, accum);
+}
+
+// ================================================================== eWise
+template <class X, class Z>
+__global__ void k_ewise_vec(int64_t n, int op, bool add, const uint64_t *__restrict__ ub, const X *__restrict__ ux,
+                            bool u_iso, const uint64_t *__restrict__ vb, const X *__restrict__ vx, bool v_iso,
+                            uint64_t *__restrict__ ob, Z *__restrict__ oz, unsigned long long *__restrict__ cnt) {
+    unsigned long long mine = 0;
+    for (int64_t base = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) & ~63LL; base < n;
+         base += (int64_t)gridDim.x * blockDim.x) {
+        int64_t i = base + (threadIdx.x & 63);
+        bool a = i < n && gb_bit(ub, i), b = i < n && gb_bit(vb, i);
+        bool have = add ? (a || b) : (a && b);
+        if (have) {
+            if (a && b) oz[i] = gb_binop_z<X, Z>(op, ux[u_iso ? 0 : i], vx[v_iso ? 0 : i], i, 0, 0);
+            else if (a) oz[i] = gb_cast<Z, X>(ux[u_iso ? 0 : i]);
+            else oz[i] = gb_cast<Z, X>(vx[v_iso ? 0 : i]);
+        }
+        unsigned long long w = __ballot(have);
+        if ((threadIdx.x & 63) == 0) {
+            ob[base >> 6] = w;
+            mine += __popcll(w);
+        }
+    }
+    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(cnt, mine);
+}
+
+template <class X, class Z, bool FILL>
+__global__ void k_ewise_mat(int64_t nrows, int op, bool add, const int64_t *__restrict__ arp,
+                            const int32_t *__restrict__ aci, const X *__restrict__ ax, bool a_iso,
+                            const int64_t *__restrict__ brp, const int32_t *__restrict__ bci, const X *__restrict__ bx,
+                            bool b_iso, int64_t *__restrict__ orp, int32_t *__restrict__ oci, Z *__restrict__ oz) {
+    OPS_STRIDE(i, nrows) {
+        int64_t pa = arp[i], ea = arp[i + 1], pb = brp[i], eb = brp[i + 1];
+        int64_t o = FILL ? orp[i] : 0;
+        while (pa < ea || pb < eb) {
+            int32_t ja = pa < ea ? aci[pa] : INT32_MAX, jb = pb < eb ? bci[pb] : INT32_MAX;
+            int32_t j = ja < jb ? ja : jb;
+            bool a = ja == j, b = jb == j;
+            bool have = add ? true : (a && b);
+            if (have) {
+                if (FILL) {
+                    oci[o] = j;
+                    if (a && b) oz[o] = gb_binop_z<X, Z>(op, ax[a_iso ? 0 : pa], bx[b_iso ? 0 : pb], i, j, j);
+                    else if (a) oz[o] = gb_cast<Z, X>(ax[a_iso ? 0 : pa]);
+                    else oz[o] = gb_cast<Z, X>(bx[b_iso ? 0 : pb]);
+                }
+                o++;
+            }
+            if (a) pa++;
+            if (b) pb++;
+        }
+        if (!FILL) orp[i] = o;
+    }
+}
+
+template <class F>
+static void dispatch_xz(int xcode, int zcode, F &&f) {
+    if (xcode == zcode) {
+        gb_with_type(xcode, [&](auto x) {
+            using X = decltype(x);
+            f(X{}, X{});
+        });
+    } else if (zcode == GBAMD_T_BOOL) {
+        gb_with_type(xcode, [&](auto x) {
+            using X = decltype(x);
+            f(X{}, bool{});
+        });
+    } else {
+        gb_throw(GrB_NOT_IMPLEMENTED, "operator type combination not supported");
+    }
+}
+
+static void do_ewise(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, GrB_BinaryOp op, GB_Obj *A, GB_Obj *B,
+                     const gb_desc &d, bool add) {
+    check_binop(op, false);
+    check_binop(accum, true);
+    GB_REQUIRE(op->xtype != nullptr, GrB_NOT_IMPLEMENTED, "positional eWise operator");
+    int xcode = op->xtype->code, zcode = op->ztype->code;
+    bool vec = C->kind != GB_KIND_MATRIX;
+    if (vec) {
+        int64_t n = C->nrows;
+        GB_REQUIRE(A->nrows == n && B->nrows == n && ncols_of(A) == 1 && ncols_of(B) == 1, GrB_DIMENSION_MISMATCH,
+                   "vector sizes do not match");
+        gb_bitmap_view ua, ub;
+        gb_get_bitmap(ua, A);
+        gb_get_bitmap(ub, B);
+        gb_scratch s;
+        const void *xa = gb_bitmap_vals_as(ua, xcode, s), *xb = gb_bitmap_vals_as(ub, xcode, s);
+        gb_vec_result T;
+        T.n = n;
+        T.tcode = zcode;
+        T.bits = gb_malloc_n<uint64_t>(gb_words(n));
+        T.dense = gb_malloc(n * gb_type_size(zcode));
+        T.d_nvals = gb_malloc_n<int64_t>(1);
+        gb_memset(T.d_nvals, 0, sizeof(int64_t));
+        dispatch_xz(xcode, zcode, [&](auto x, auto z) {
+            using X = decltype(x);
+            using Z = decltype(z);
+            if (n)
+                hipLaunchKernelGGL((k_ewise_vec<X, Z>), dim3(ops_grid(n)), dim3(OPS_BLOCK), 0, gb_stream(), n,
+                                   op->opcode, add, ua.bits, (const X *)xa, ua.iso, ub.bits, (const X *)xb, ub.iso,
+                                   T.bits, (Z *)T.dense, (unsigned long long *)T.d_nvals);
+        });
+        GB_LAUNCH_CHECK();
+        gb_writeback_vector(C, T, M, d, accum, false);
+        return;
+    }
+    int64_t nr = C->nrows, nc = C->ncols;
+    GB_Obj *A2 = A, *B2 = B;
+    gb_csr_view av, bv;
+    if (d.tran0) gb_get_csc(av, A2);
+    else gb_get_csr(av, A2);
+    if (d.tran1) gb_get_csc(bv, B2);
+    else gb_get_csr(bv, B2);
+    GB_REQUIRE(av.nrows == nr && av.ncols == nc && bv.nrows == nr && bv.ncols == nc, GrB_DIMENSION_MISMATCH,
+               "matrix dimensions do not match");
+    gb_scratch s;
+    const void *xa = gb_view_vals_as(av, xcode, s), *xb = gb_view_vals_as(bv, xcode, s);
+    gb_mat_result T;
+    T.nrows = nr;
+    T.ncols = nc;
+    T.tcode = zcode;
+    int64_t *cnt = s.get<int64_t>(nr + 1);
+    T.rowptr = gb_malloc_n<int64_t>(nr + 1);
+    dispatch_xz(xcode, zcode, [&](auto x, auto z) {
+        using X = decltype(x);
+        using Z = decltype(z);
+        if (nr)
+            hipLaunchKernelGGL((k_ewise_mat<X, Z, false>), dim3(ops_grid(nr)), dim3(OPS_BLOCK), 0, gb_stream(), nr,
+                               op->opcode, add, av.rowptr, av.colidx, (const X *)xa, av.iso, bv.rowptr, bv.colidx,
+                               (const X *)xb, bv.iso, cnt, nullptr, nullptr);
+        GB_LAUNCH_CHECK();
+        gb_exclusive_scan_i64(cnt, T.rowptr, nr);
+        T.nvals = gb_read_i64(T.rowptr + nr);
+        T.colidx = gb_malloc_n<int32_t>(T.nvals);
+        T.vals = gb_malloc(T.nvals * sizeof(Z));
+        if (nr)
+            hipLaunchKernelGGL((k_ewise_mat<X, Z, true>), dim3(ops_grid(nr)), dim3(OPS_BLOCK), 0, gb_stream(), nr,
+                               op->opcode, add, av.rowptr, av.colidx, (const X *)xa, av.iso, bv.rowptr, bv.colidx,
+                               (const X *)xb, bv.iso, T.rowptr, T.colidx, (Z *)T.vals);
+        GB_LAUNCH_CHECK();
+    });
+    gb_writeback_matrix(C, T, M, d, accum);
+}
+
+// ================================================================== reduce
+template <class T>
+__global__ void k_reduce_partial(int mon, const T *__restrict__ vals, bool iso, int64_t nvals,
+                                 const uint64_t *__restrict__ bits, int64_t n, T *__restrict__ part,
+                                 int *__restrict__ pfound) {
+    // bits == nullptr: reduce vals[0..nvals); else reduce vals[i] for set bits i < n
+    __shared__ T sv[256];
+    __shared__ int sf[256];
+    T acc = T();
+    bool found = false;
+    int64_t total = bits ? n : nvals;
+    OPS_STRIDE(i, total) {
+        if (bits && !gb_bit(bits, i)) continue;
+        T v = vals[iso ? 0 : i];
+        acc = found ? gb_monoid<T>(mon, acc, v) : v;
+        found = true;
+    }
+    sv[threadIdx.x] = acc;
+    sf[threadIdx.x] = found;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T a = T();
+        bool f = false;
+        for (int t = 0; t < blockDim.x; t++)
+            if (sf[t]) {
+                a = f ? gb_monoid<T>(mon, a, sv[t]) : sv[t];
+                f = true;
+            }
+        part[blockIdx.x] = a;
+        pfound[blockIdx.x] = f;
+    }
+}
+
+// returns true if any entry; value in *out (monoid type)
+static bool reduce_values(GB_Obj *A, GrB_Monoid monoid, void *out) {
+    GB_REQUIRE(monoid && monoid->magic == GB_MAGIC, GrB_UNINITIALIZED_OBJECT, "invalid monoid");
+    int code = monoid->type->code;
+    gb_scratch s;
+    const void *vals;
+    bool iso;
+    const uint64_t *bits = nullptr;
+    int64_t n, nvals;
+    gb_bitmap_view bv;
+    gb_csr_view cv;
+    if (A->kind == GB_KIND_MATRIX) {
+        gb_get_csr(cv, A);
+        vals = gb_view_vals_as(cv, code, s);
+        iso = cv.iso;
+        nvals = cv.nvals;
+        n = nvals;
+    } else {
+        gb_get_bitmap(bv, A);
+        vals = gb_bitmap_vals_as(bv, code, s);
+        iso = bv.iso;
+        bits = bv.bits;
+        n = bv.n;
+        nvals = n;
+    }
+    const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(256, (n + 255) / 256));
+    bool any = false;
+    gb_with_type(code, [&](auto z) {
+        using T = decltype(z);
+        T *part = s.get<T>(nb);
+        int *pf = s.get<int>(nb);
+        hipLaunchKernelGGL(k_reduce_partial<T>, dim3(nb), dim3(256), 0, gb_stream(), monoid->mcode, (const T *)vals,
+                           iso, nvals, bits, n, part, pf);
+        GB_LAUNCH_CHECK();
+        std::vector<char> hpb(nb * sizeof(T));
+        std::vector<int> hf(nb);
+        gb_copy_d2h(hpb.data(), part, nb * sizeof(T));
+        gb_copy_d2h(hf.data(), pf, nb * sizeof(int));
+        T acc = T();
+        for (int b = 0; b < nb; b++)
+            if (hf[b]) {
+                T hv;
+                memcpy(&hv, hpb.data() + b * sizeof(T), sizeof(T));
+                acc = any ? gb_monoid<T>(monoid->mcode, acc, hv) : hv;
+                any = true;
+            }
+        memcpy(out, &acc, sizeof(T));
+    });
+    return any;
+}
+
+// identity of a monoid (value written to *out)
+static void monoid_identity(GrB_Monoid monoid, void *out) {
+    int m = monoid->mcode;
+    gb_with_type(monoid->type->code, [&](auto z) {
+        using T = decltype(z);
+        T v = T();
+        switch (m) {
+        case GBAMD_MON_TIMES: v = (T)1; break;
+        case GBAMD_MON_MIN: v = gb_tmax<T>(); break;
+        case GBAMD_MON_MAX: v = gb_tmin<T>(); break;
+        case GBAMD_MON_LAND: case GBAMD_MON_LXNOR: v = (T)1; break;
+        case GBAMD_MON_BAND: case GBAMD_MON_BXNOR:
+            if constexpr (gb_traits<T>::is_int) v = (T)~(T)0;
+            break;
+        default: v = T(); break;
+        }
+        memcpy(out, &v, sizeof(T));
+    });
+}
+
+// ================================================================== transpose
+static void do_transpose(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, GB_Obj *A, const gb_desc &d) {
+    check_binop(accum, true);
+    gb_csr_view v;
+    if (d.tran0) gb_get_csr(v, A);  // transpose of the transpose
+    else gb_get_csc(v, A);
+    gb_mat_result T;
+    T.nrows = v.nrows;
+    T.ncols = v.ncols;
+    T.nvals = v.nvals;
+    T.tcode = v.tcode;
+    T.iso = v.iso;
+    size_t ts = gb_type_size(v.tcode);
+    T.rowptr = gb_malloc_n<int64_t>(v.nrows + 1);
+    gb_copy_d2d(T.rowptr, v.rowptr, (v.nrows + 1) * sizeof(int64_t));
+    T.colidx = gb_malloc_n<int32_t>(v.nvals);
+    gb_copy_d2d(T.colidx, v.colidx, v.nvals * sizeof(int32_t));
+    int64_t nv = v.iso ? 1 : v.nvals;
+    T.vals = gb_malloc(nv * ts);
+    gb_copy_d2d(T.vals, v.vals, nv * ts);
+    gb_writeback_matrix(C, T, M, d, accum);
+}
+
+// ================================================================== assign
+// T for "x assigned at every index of I (GrB_ALL: all)": iso bitmap vector
+static void scalar_vec_T(gb_vec_result &T, int64_t n, const GrB_Index *I, int64_t ni, const void *x, int code) {
+    T.n = n;
+    T.tcode = code;
+    T.iso = true;
+    int64_t nw = gb_words(n);
+    T.bits = gb_malloc_n<uint64_t>(nw);
+    T.dense = gb_malloc(gb_type_size(code));
+    gb_copy_h2d(T.dense, x, gb_type_size(code));
+    T.d_nvals = gb_malloc_n<int64_t>(1);
+    if (I == GrB_ALL) {
+        std::vector<uint64_t> hb(nw, ~0ULL);
+        if (n & 63) hb[nw - 1] = (1ULL << (n & 63)) - 1;
+        gb_copy_h2d(T.bits, hb.data(), nw * sizeof(uint64_t));
+        int64_t nn = n;
+        gb_copy_h2d(T.d_nvals, &nn, sizeof(int64_t));
+        gb_sync();
+        return;
+    }
+    std::vector<uint64_t> hb(nw, 0);
+    int64_t c = 0;
+    for (int64_t q = 0; q < ni; q++) {
+        GB_REQUIRE(I[q] < (GrB_Index)n, GrB_INDEX_OUT_OF_BOUNDS, "assign index out of bounds");
+        uint64_t &w = hb[I[q] >> 6];
+        uint64_t b = 1ULL << (I[q] & 63);
+        if (!(w & b)) c++;
+        w |= b;
+    }
+    gb_copy_h2d(T.bits, hb.data(), nw * sizeof(uint64_t));
+    gb_copy_h2d(T.d_nvals, &c, sizeof(int64_t));
+    gb_sync();
+}
+
+static GrB_BinaryOp second_of(int code) {
+    void *h;
+    int kind;
+    std::string name = std::string("GrB_SECOND_") + gb_type_name(code);
+    GxB_builtin_lookup(&h, &kind, name.c_str());
+    return (GrB_BinaryOp)h;
+}
+
+static void vector_assign_scalar(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, const void *x, int xcode,
+                                 const GrB_Index *I, int64_t ni, const gb_desc &d) {
+    check_binop(accum, true);
+    GB_REQUIRE(w->kind != GB_KIND_MATRIX || w->ncols == 1, GrB_DIMENSION_MISMATCH, "not a vector");
+    int ct = w->type->code;
+    // cast the scalar to C's type on the host
+    char xc[16];
+    gb_with_type(ct, [&](auto z) {
+        using D = decltype(z);
+        gb_with_type(xcode, [&](auto y) {
+            using S = decltype(y);
+            S sv;
+            memcpy(&sv, x, sizeof(S));
+            D dv = gb_cast<D, S>(sv);
+            memcpy(xc, &dv, sizeof(D));
+        });
+    });
+    gb_vec_result T;
+    scalar_vec_T(T, w->nrows, I, ni, xc, ct);
+    GrB_BinaryOp acc = accum;
+    if (I != GrB_ALL && !acc) acc = second_of(ct);  // outside I, C is kept
+    gb_writeback_vector(w, T, mask, d, acc, false);
+}
+
+static void matrix_assign_scalar(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, const void *x, int xcode,
+                                 const GrB_Index *I, int64_t ni, const GrB_Index *J, int64_t nj, const gb_desc &d) {
+    check_binop(accum, true);
+    int ct = C->type->code;
+    char xc[16];
+    gb_with_type(ct, [&](auto z) {
+        using D = decltype(z);
+        gb_with_type(xcode, [&](auto y) {
+            using S = decltype(y);
+            S sv;
+            memcpy(&sv, x, sizeof(S));
+            D dv = gb_cast<D, S>(sv);
+            memcpy(xc, &dv, sizeof(D));
+        });
+    });
+    int64_t nr = C->nrows, nc = ncols_of(C);
+    std::vector<GrB_Index> rows, cols;
+    if (I == GrB_ALL) {
+        rows.resize(nr);
+        for (int64_t i = 0; i < nr; i++) rows[i] = i;
+    } else rows.assign(I, I + ni);
+    if (J == GrB_ALL) {
+        cols.resize(nc);
+        for (int64_t j = 0; j < nc; j++) cols[j] = j;
+    } else cols.assign(J, J + nj);
+    std::sort(rows.begin(), rows.end());
+    rows.erase(std::unique(rows.begin(), rows.end()), rows.end());
+    std::sort(cols.begin(), cols.end());
+    cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
+    for (auto r : rows) GB_REQUIRE(r < (GrB_Index)nr, GrB_INDEX_OUT_OF_BOUNDS, "row index out of bounds");
+    for (auto c : cols) GB_REQUIRE(c < (GrB_Index)nc, GrB_INDEX_OUT_OF_BOUNDS, "column index out of bounds");
+    int64_t nz = (int64_t)rows.size() * (int64_t)cols.size();
+    std::vector<int64_t> rp(nr + 1, 0);
+    for (auto r : rows) rp[r + 1] = (int64_t)cols.size();
+    for (int64_t i = 0; i < nr; i++) rp[i + 1] += rp[i];
+    std::vector<int32_t> ci(nz);
+    for (size_t a = 0; a < rows.size(); a++)
+        for (size_t b = 0; b < cols.size(); b++) ci[a * cols.size() + b] = (int32_t)cols[b];
+    gb_mat_result T;
+    T.nrows = nr;
+    T.ncols = nc;
+    T.nvals = nz;
+    T.tcode = ct;
+    T.iso = true;
+    T.rowptr = gb_malloc_n<int64_t>(nr + 1);
+    T.colidx = gb_malloc_n<int32_t>(nz);
+    T.vals = gb_malloc(gb_type_size(ct));
+    gb_copy_h2d(T.rowptr, rp.data(), (nr + 1) * sizeof(int64_t));
+    gb_copy_h2d(T.colidx, ci.data(), nz * sizeof(int32_t));
+    gb_copy_h2d(T.vals, xc, gb_type_size(ct));
+    gb_sync();
+    GrB_BinaryOp acc = accum;
+    if ((I != GrB_ALL || J != GrB_ALL) && !acc) acc = second_of(ct);
+    gb_writeback_matrix(C, T, M, d, acc);
+}
+
+// ================================================================== C API
+extern "C" {
+
+GrB_Info GrB_mxm(GrB_Matrix C, const GrB_Matrix Mask, const GrB_BinaryOp accum, const GrB_Semiring op,
+                 const GrB_Matrix A, const GrB_Matrix B, const GrB_Descriptor desc) {
+    return gb_api(OBJ(C), [&] {
+        do_mxm(gb_obj_check(C), gb_obj_check(Mask, true), accum, op, gb_obj_check(A), gb_obj_check(B),
+               gb_read_desc(desc));
+    });
+}
+
+GrB_Info GrB_mxv(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum, const GrB_Semiring op,
+                 const GrB_Matrix A, const GrB_Vector u, const GrB_Descriptor desc) {
+    return gb_api(OBJ(w), [&] {
+        do_spmv(gb_obj_check(w), gb_obj_check(mask, true), accum, op, gb_obj_check(A), gb_obj_check(u),
+                gb_read_desc(desc), false);
+    });
+}
+
+GrB_Info GrB_vxm(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum, const GrB_Semiring op,
+                 const GrB_Vector u, const GrB_Matrix A, const GrB_Descriptor desc) {
+    return gb_api(OBJ(w), [&] {
+        do_spmv(gb_obj_check(w), gb_obj_check(mask, true), accum, op, gb_obj_check(A), gb_obj_check(u),
+                gb_read_desc(desc), true);
+    });
+}
+
+GrB_Info GrB_Matrix_eWiseMult_BinaryOp(GrB_Matrix C, const GrB_Matrix Mask, const GrB_BinaryOp accum,
+                                       const GrB_BinaryOp op, const GrB_Matrix A, const GrB_Matrix B,
+                                       const GrB_Descriptor desc) {
+    return gb_api(OBJ(C), [&] {
+        do_ewise(gb_obj_check(C), gb_obj_check(Mask, true), accum, op, gb_obj_check(A), gb_obj_check(B),
+                 gb_read_desc(desc), false);
+    });
+}
+GrB_Info GrB_Vector_eWiseMult_BinaryOp(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum,
+                                       const GrB_BinaryOp op, const GrB_Vector u, const GrB_Vector v,
+                                       const GrB_Descriptor desc) {
+    return gb_api(OBJ(w), [&] {
+        do_ewise(gb_obj_check(w), gb_obj_check(mask, true), accum, op, gb_obj_check(u), gb_obj_check(v),
+                 gb_read_desc(desc), false);
+    });
+}
+GrB_Info GrB_Matrix_eWiseAdd_BinaryOp(GrB_Matrix C, const GrB_Matrix Mask, const GrB_BinaryOp accum,
+                                      const GrB_BinaryOp op, const GrB_Matrix A, const GrB_Matrix B,
+                                      const GrB_Descriptor desc) {
+    return gb_api(OBJ(C), [&] {
+        do_ewise(gb_obj_check(C), gb_obj_check(Mask, true), accum, op, gb_obj_check(A), gb_obj_check(B),
+                 gb_read_desc(desc), true);
+    });
+}
+GrB_Info GrB_Vector_eWiseAdd_BinaryOp(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum,
+                                      const GrB_BinaryOp op, const GrB_Vector u, const GrB_Vector v,
+                                      const GrB_Descriptor desc) {
+    return gb_api(OBJ(w), [&] {
+        do_ewise(gb_obj_check(w), gb_obj_check(mask, true), accum, op, gb_obj_check(u), gb_obj_check(v),
+                 gb_read_desc(desc), true);
+    });
+}
+
+GrB_Info GrB_transpose(GrB_Matrix C, const GrB_Matrix Mask, const GrB_BinaryOp accum, const GrB_Matrix A,
+                       const GrB_Descriptor desc) {
+    return gb_api(OBJ(C), [&] {
+        do_transpose(gb_obj_check(C), gb_obj_check(Mask, true), accum, gb_obj_check(A), gb_read_desc(desc));
+    });
+}
+
+GrB_Info GrB_Vector_assign(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum, const GrB_Vector u,
+                           const GrB_Index *I, GrB_Index ni, const GrB_Descriptor desc) {
+    return gb_api(OBJ(w), [&] {
+        GB_Obj *W = gb_obj_check(w), *U = gb_obj_check(u);
+        gb_desc d = gb_read_desc(desc);
+        check_binop(accum, true);
+        int64_t n = W->nrows;
+        gb_vec_result T;
+        T.n = n;
+        T.tcode = U->type->code;
+        if (I == GrB_ALL) {
+            GB_REQUIRE(U->nrows == n, GrB_DIMENSION_MISMATCH, "u size does not match w");
+            gb_bitmap_view uv;
+            gb_get_bitmap(uv, U);
+            T.iso = uv.iso;
+            T.bits = gb_malloc_n<uint64_t>(gb_words(n));
+            gb_copy_d2d(T.bits, uv.bits, gb_words(n) * sizeof(uint64_t));
+            size_t ts = gb_type_size(uv.tcode);
+            T.dense = gb_malloc((uv.iso ? 1 : n) * ts);
+            gb_copy_d2d(T.dense, uv.vals, (uv.iso ? 1 : n) * ts);
+            T.d_nvals = gb_malloc_n<int64_t>(1);
+            gb_bitmap_count(T.bits, n, T.d_nvals);
+            gb_writeback_vector(W, T, gb_obj_check(mask, true), d, accum, false);
+            return;
+        }
+        // index list: w(I[k]) = u(k)
+        GB_REQUIRE((GrB_Index)U->nrows == ni, GrB_DIMENSION_MISMATCH, "u size does not match the index list");
+        int64_t unv = gb_nvals(U);
+        std::vector<GrB_Index> ui(unv);
+        std::vector<char> ux(unv * U->type->size);
+        {
+            GrB_Index nv = unv;
+            gb_extract_tuples(U, ui.data(), nullptr, ux.data(), U->type->code, &nv);
+        }
+        GB_Obj *Tv = gb_new_object(GB_KIND_VECTOR, U->type, n, 1);
+        std::vector<GrB_Index> wi(unv);
+        for (int64_t q = 0; q < unv; q++) {
+            GB_REQUIRE(ui[q] < ni && I[ui[q]] < (GrB_Index)n, GrB_INDEX_OUT_OF_BOUNDS, "index out of bounds");
+            wi[q] = I[ui[q]];
+        }
+        try {
+            gb_build(Tv, wi.data(), nullptr, ux.data(), U->type->code, false, unv, nullptr);
+        } catch (...) {
+            GrB_Vector tv = (GrB_Vector)Tv;
+            GrB_Vector_free(&tv);
+            throw;
+        }
+        gb_bitmap_view tvw;
+        gb_get_bitmap(tvw, Tv);
+        T.iso = tvw.iso;
+        T.bits = gb_malloc_n<uint64_t>(gb_words(n));
+        gb_copy_d2d(T.bits, tvw.bits, gb_words(n) * sizeof(uint64_t));
+        size_t ts = gb_type_size(tvw.tcode);
+        T.dense = gb_malloc((tvw.iso ? 1 : n) * ts);
+        gb_copy_d2d(T.dense, tvw.vals, (tvw.iso ? 1 : n) * ts);
+        T.d_nvals = gb_malloc_n<int64_t>(1);
+        gb_bitmap_count(T.bits, n, T.d_nvals);
+        GrB_Vector tv = (GrB_Vector)Tv;
+        GrB_Vector_free(&tv);
+        gb_writeback_vector(W, T, gb_obj_check(mask, true), d, accum ? accum : second_of(W->type->code), false);
+    });
+}
+
+GrB_Info GrB_Matrix_assign(GrB_Matrix C, const GrB_Matrix Mask, const GrB_BinaryOp accum, const GrB_Matrix A,
+                           const GrB_Index *I, GrB_Index ni, const GrB_Index *J, GrB_Index nj,
+                           const GrB_Descriptor desc) {
+    return gb_api(OBJ(C), [&] {
+        GB_Obj *Co = gb_obj_check(C), *Ao = gb_obj_check(A);
+        gb_desc d = gb_read_desc(desc);
+        GB_REQUIRE(I == GrB_ALL && J == GrB_ALL, GrB_NOT_IMPLEMENTED, "Matrix_assign supports GrB_ALL only");
+        gb_csr_view v;
+        if (d.tran0) gb_get_csc(v, Ao);
+        else gb_get_csr(v, Ao);
+        GB_REQUIRE(v.nrows == Co->nrows && v.ncols == ncols_of(Co), GrB_DIMENSION_MISMATCH, "dimension mismatch");
+        gb_mat_result T;
+        T.nrows = v.nrows;
+        T.ncols = v.ncols;
+        T.nvals = v.nvals;
+        T.tcode = v.tcode;
+        T.iso = v.iso;
+        size_t ts = gb_type_size(v.tcode);
+        T.rowptr = gb_malloc_n<int64_t>(v.nrows + 1);
+        gb_copy_d2d(T.rowptr, v.rowptr, (v.nrows + 1) * sizeof(int64_t));
+        T.colidx = gb_malloc_n<int32_t>(v.nvals);
+        gb_copy_d2d(T.colidx, v.colidx, v.nvals * sizeof(int32_t));
+        T.vals = gb_malloc((v.iso ? 1 : v.nvals) * ts);
+        gb_copy_d2d(T.vals, v.vals, (v.iso ? 1 : v.nvals) * ts);
+        gb_writeback_matrix(Co, T, gb_obj_check(Mask, true), d, accum);
+    });
+}
+
+GrB_Info GrB_Matrix_reduce_Monoid_Scalar(GrB_Scalar s, const GrB_BinaryOp accum, const GrB_Monoid monoid,
+                                         const GrB_Matrix A, const GrB_Descriptor desc) {
+    (void)desc;
+    return gb_api(OBJ(s), [&] {
+        GB_Obj *S = gb_obj_check(s);
+        char v[16];
+        bool any = reduce_values(gb_obj_check(A), monoid, v);
+        gb_vec_result T;
+        T.n = 1;
+        T.tcode = monoid->type->code;
+        T.iso = true;
+        T.bits = gb_malloc_n<uint64_t>(1);
+        uint64_t b = any ? 1 : 0;
+        gb_copy_h2d(T.bits, &b, sizeof(b));
+        T.dense = gb_malloc(16);
+        gb_copy_h2d(T.dense, v, gb_type_size(T.tcode));
+        T.d_nvals = gb_malloc_n<int64_t>(1);
+        int64_t nn = any ? 1 : 0;
+        gb_copy_h2d(T.d_nvals, &nn, sizeof(nn));
+        gb_sync();
+        gb_writeback_vector(S, T, nullptr, gb_desc(), accum, false);
+    });
+}
+GrB_Info GrB_Vector_reduce_Monoid_Scalar(GrB_Scalar s, const GrB_BinaryOp accum, const GrB_Monoid monoid,
+                                         const GrB_Vector u, const GrB_Descriptor desc) {
+    return GrB_Matrix_reduce_Monoid_Scalar(s, accum, monoid, (GrB_Matrix)u, desc);
+}
+
+#define GB_DEFINE_TYPED_OPS(T, ctype)                                                                          \
+    GrB_Info GrB_Vector_assign_##T(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum, ctype x,   \
+                                   const GrB_Index *I, GrB_Index ni, const GrB_Descriptor desc) {            \
+        return gb_api(OBJ(w), [&] {                                                                          \
+            vector_assign_scalar(gb_obj_check(w), gb_obj_check(mask, true), accum, &x, GBAMD_T_##T, I,       \
+                                 (int64_t)ni, gb_read_desc(desc));                                           \
+        });                                                                                                  \
+    }                                                                                                        \
+    GrB_Info GrB_Matrix_assign_##T(GrB_Matrix C, const GrB_Matrix Mask, const GrB_BinaryOp accum, ctype x,   \
+                                   const GrB_Index *I, GrB_Index ni, const GrB_Index *J, GrB_Index nj,       \
+                                   const GrB_Descriptor desc) {                                              \
+        return gb_api(OBJ(C), [&] {                                                                          \
+            GB_Obj *Co = gb_obj_check(C);                                                                    \
+            if (Co->kind != GB_KIND_MATRIX)                                                                  \
+                vector_assign_scalar(Co, gb_obj_check(Mask, true), accum, &x, GBAMD_T_##T, I, (int64_t)ni,   \
+                                     gb_read_desc(desc));                                                    \
+            else                                                                                             \
+                matrix_assign_scalar(Co, gb_obj_check(Mask, true), accum, &x, GBAMD_T_##T, I, (int64_t)ni, J, \
+                                     (int64_t)nj, gb_read_desc(desc));                                       \
+        });                                                                                                  \
+    }                                                                                                        \
+    GrB_Info GrB_Vector_reduce_##T(ctype *c, const GrB_BinaryOp accum, const GrB_Monoid monoid,              \
+                                   const GrB_Vector u, const GrB_Descriptor desc) {                          \
+        (void)desc;                                                                                          \
+        if (!c) return GrB_NULL_POINTER;                                                                     \
+        return gb_api(OBJ(u), [&] {                                                                          \
+            char v[16];                                                                                      \
+            GB_REQUIRE(monoid && monoid->magic == GB_MAGIC, GrB_UNINITIALIZED_OBJECT, "invalid monoid");     \
+            if (!reduce_values(gb_obj_check(u), monoid, v)) monoid_identity(monoid, v);                      \
+            ctype r;                                                                                         \
+            gb_with_type(monoid->type->code, [&](auto z) {                                                   \
+                using S = decltype(z);                                                                       \
+                S sv;                                                                                        \
+                memcpy(&sv, v, sizeof(S));                                                                   \
+                r = gb_cast<ctype, S>(sv);                                                                   \
+            });                                                                                              \
+            if (accum) {                                                                                     \
+                check_binop(accum, false);                                                                   \
+                r = gb_binop<ctype>(accum->opcode, *c, r);                                                   \
+            }                                                                                                \
+            *c = r;                                                                                          \
+        });                                                                                                  \
+    }                                                                                                        \
+    GrB_Info GrB_Matrix_reduce_##T(ctype *c, const GrB_BinaryOp accum, const GrB_Monoid monoid,              \
+                                   const GrB_Matrix A, const GrB_Descriptor desc) {                          \
+        return GrB_Vector_reduce_##T(c, accum, monoid, (GrB_Vector)A, desc);                                 \
+    }
+
+GB_FOR_EACH_TYPE(GB_DEFINE_TYPED_OPS)
+
+}  // extern "C"

@@ -1,0 +1,378 @@
+// gb_prim.hip -- device primitives shared by the kernels: scans, radix sorts
+// (rocPRIM through hipCUB, used only on ingest / format conversion paths),
+// typecasts, bitmap <-> CSR conversion, CSR transpose.
+#include <hipcub/hipcub.hpp>
+
+#include "gb_device.cuh"
+#include "gb_internal.h"
+
+#define GB_BLOCK 256
+
+static inline unsigned gb_grid(int64_t n, int per_block = GB_BLOCK) {
+    int64_t g = (n + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > (1LL << 30)) g = 1LL << 30;
+    return (unsigned)g;
+}
+
+// ------------------------------------------------------------------ scans / sorts
+void gb_exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n) {
+    // out has n+1 slots: out[0] = 0, out[i+1] = in[0] + ... + in[i]
+    gb_memset(out, 0, sizeof(int64_t));
+    if (n == 0) return;
+    GB_REQUIRE(n < (1LL << 31), GrB_NOT_IMPLEMENTED, "scan of more than 2^31 items");
+    size_t tmp = 0;
+    GB_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tmp, in, out + 1, (int)n, gb_stream()));
+    void *t = gb_malloc(tmp);
+    GB_HIP(hipcub::DeviceScan::InclusiveSum(t, tmp, in, out + 1, (int)n, gb_stream()));
+    gb_free(t);
+}
+
+__global__ void k_iota(int64_t *x, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        x[i] = i;
+}
+
+__global__ void k_copy_i64(int64_t *dst, const int64_t *src) { *dst = *src; }
+
+void gb_sort_pairs_u64(uint64_t *keys, int64_t *vals, int64_t n, int end_bit) {
+    if (n <= 1) return;
+    GB_REQUIRE(n < (1LL << 31), GrB_NOT_IMPLEMENTED, "sort of more than 2^31 items");
+    uint64_t *k2 = gb_malloc_n<uint64_t>(n);
+    int64_t *v2 = gb_malloc_n<int64_t>(n);
+    hipcub::DoubleBuffer<uint64_t> kb(keys, k2);
+    hipcub::DoubleBuffer<int64_t> vb(vals, v2);
+    size_t tmp = 0;
+    GB_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, kb, vb, (int)n, 0, end_bit, gb_stream()));
+    void *t = gb_malloc(tmp);
+    GB_HIP(hipcub::DeviceRadixSort::SortPairs(t, tmp, kb, vb, (int)n, 0, end_bit, gb_stream()));
+    if (kb.Current() != keys) gb_copy_d2d(keys, kb.Current(), n * sizeof(uint64_t));
+    if (vb.Current() != vals) gb_copy_d2d(vals, vb.Current(), n * sizeof(int64_t));
+    gb_free(t);
+    gb_free(k2);
+    gb_free(v2);
+}
+
+void gb_sort_pairs_i32(int32_t *keys, int64_t *vals, int64_t n, int end_bit) {
+    if (n <= 1) return;
+    GB_REQUIRE(n < (1LL << 31), GrB_NOT_IMPLEMENTED, "sort of more than 2^31 items");
+    int32_t *k2 = gb_malloc_n<int32_t>(n);
+    int64_t *v2 = gb_malloc_n<int64_t>(n);
+    hipcub::DoubleBuffer<int32_t> kb(keys, k2);
+    hipcub::DoubleBuffer<int64_t> vb(vals, v2);
+    size_t tmp = 0;
+    GB_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, kb, vb, (int)n, 0, end_bit, gb_stream()));
+    void *t = gb_malloc(tmp);
+    GB_HIP(hipcub::DeviceRadixSort::SortPairs(t, tmp, kb, vb, (int)n, 0, end_bit, gb_stream()));
+    if (kb.Current() != keys) gb_copy_d2d(keys, kb.Current(), n * sizeof(int32_t));
+    if (vb.Current() != vals) gb_copy_d2d(vals, vb.Current(), n * sizeof(int64_t));
+    gb_free(t);
+    gb_free(k2);
+    gb_free(v2);
+}
+
+// ------------------------------------------------------------------ casts
+template <class D, class S>
+__global__ void k_cast(D *__restrict__ dst, const S *__restrict__ src, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = gb_cast<D, S>(src[i]);
+}
+
+template <class D>
+static void cast_from(void *dst, const void *src, int src_code, int64_t n) {
+    unsigned g = gb_grid(n);
+    if (g > 4096) g = 4096;
+#define GB_CASE(code, S)                                                                        \
+    case code:                                                                                  \
+        hipLaunchKernelGGL((k_cast<D, S>), dim3(g), dim3(GB_BLOCK), 0, gb_stream(), (D *)dst, \
+                           (const S *)src, n);                                                  \
+        break;
+    switch (src_code) {
+        GB_CASE(GBAMD_T_BOOL, bool)
+        GB_CASE(GBAMD_T_INT8, int8_t)
+        GB_CASE(GBAMD_T_UINT8, uint8_t)
+        GB_CASE(GBAMD_T_INT16, int16_t)
+        GB_CASE(GBAMD_T_UINT16, uint16_t)
+        GB_CASE(GBAMD_T_INT32, int32_t)
+        GB_CASE(GBAMD_T_UINT32, uint32_t)
+        GB_CASE(GBAMD_T_INT64, int64_t)
+        GB_CASE(GBAMD_T_UINT64, uint64_t)
+        GB_CASE(GBAMD_T_FP32, float)
+        GB_CASE(GBAMD_T_FP64, double)
+    }
+#undef GB_CASE
+    GB_LAUNCH_CHECK();
+}
+
+void gb_cast_array(void *dst, int dst_code, const void *src, int src_code, int64_t n) {
+    if (n <= 0) return;
+    if (dst_code == src_code) {
+        gb_copy_d2d(dst, src, n * gb_type_size(dst_code));
+        return;
+    }
+    switch (dst_code) {
+    case GBAMD_T_BOOL: cast_from<bool>(dst, src, src_code, n); break;
+    case GBAMD_T_INT8: cast_from<int8_t>(dst, src, src_code, n); break;
+    case GBAMD_T_UINT8: cast_from<uint8_t>(dst, src, src_code, n); break;
+    case GBAMD_T_INT16: cast_from<int16_t>(dst, src, src_code, n); break;
+    case GBAMD_T_UINT16: cast_from<uint16_t>(dst, src, src_code, n); break;
+    case GBAMD_T_INT32: cast_from<int32_t>(dst, src, src_code, n); break;
+    case GBAMD_T_UINT32: cast_from<uint32_t>(dst, src, src_code, n); break;
+    case GBAMD_T_INT64: cast_from<int64_t>(dst, src, src_code, n); break;
+    case GBAMD_T_UINT64: cast_from<uint64_t>(dst, src, src_code, n); break;
+    case GBAMD_T_FP32: cast_from<float>(dst, src, src_code, n); break;
+    case GBAMD_T_FP64: cast_from<double>(dst, src, src_code, n); break;
+    }
+}
+
+// ------------------------------------------------------------------ iso expansion
+template <class W>
+__global__ void k_fill(W *__restrict__ dst, const W *__restrict__ one, int64_t n) {
+    W v = *one;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = v;
+}
+
+void *gb_expand_iso(const void *one_value, size_t tsize, int64_t n) {
+    void *out = gb_malloc(n * tsize);
+    if (n == 0) return out;
+    unsigned g = gb_grid(n);
+    if (g > 4096) g = 4096;
+    switch (tsize) {
+    case 1: hipLaunchKernelGGL(k_fill<uint8_t>, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), (uint8_t *)out, (const uint8_t *)one_value, n); break;
+    case 2: hipLaunchKernelGGL(k_fill<uint16_t>, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), (uint16_t *)out, (const uint16_t *)one_value, n); break;
+    case 4: hipLaunchKernelGGL(k_fill<uint32_t>, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), (uint32_t *)out, (const uint32_t *)one_value, n); break;
+    default: hipLaunchKernelGGL(k_fill<uint64_t>, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), (uint64_t *)out, (const uint64_t *)one_value, n); break;
+    }
+    GB_LAUNCH_CHECK();
+    return out;
+}
+
+// ------------------------------------------------------------------ bitmap helpers
+// one 64-bit word per lane; wave-level popcount reduction, one atomic per block
+__global__ void k_bitmap_count(const uint64_t *__restrict__ bits, int64_t nwords,
+                               unsigned long long *__restrict__ count) {
+    __shared__ unsigned long long part;
+    if (threadIdx.x == 0) part = 0;
+    __syncthreads();
+    unsigned long long c = 0;
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nwords;
+         w += (int64_t)gridDim.x * blockDim.x)
+        c += __popcll(bits[w]);
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&part, c);
+    __syncthreads();
+    if (threadIdx.x == 0 && part) atomicAdd(count, part);
+}
+
+void gb_bitmap_count(const uint64_t *bits, int64_t n, int64_t *d_count) {
+    gb_memset(d_count, 0, sizeof(int64_t));
+    int64_t nw = gb_words(n);
+    if (nw == 0) return;
+    unsigned g = gb_grid(nw);
+    if (g > 1024) g = 1024;
+    hipLaunchKernelGGL(k_bitmap_count, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), bits, nw,
+                       (unsigned long long *)d_count);
+    GB_LAUNCH_CHECK();
+}
+
+// per-word popcount -> exclusive scan -> positions
+__global__ void k_word_pop(const uint64_t *__restrict__ bits, int64_t nwords, int64_t *__restrict__ pop) {
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nwords;
+         w += (int64_t)gridDim.x * blockDim.x)
+        pop[w] = __popcll(bits[w]);
+}
+
+template <class W>
+__global__ void k_bitmap_scatter(const uint64_t *__restrict__ bits, const W *__restrict__ dense,
+                                 bool iso, int64_t n, const int64_t *__restrict__ woff,
+                                 int64_t *__restrict__ rowptr_n1, int32_t *__restrict__ colidx,
+                                 W *__restrict__ vals) {
+    // n x 1 CSR: row i has one entry (col 0) iff bit i set.  rowptr[i] = rank(i).
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t w = bits[i >> 6];
+        int b = i & 63;
+        int64_t rank = woff[i >> 6] + __popcll(w & ((b == 0) ? 0ULL : (~0ULL >> (64 - b))));
+        rowptr_n1[i] = rank;
+        if ((w >> b) & 1ULL) {
+            colidx[rank] = 0;
+            if (vals) vals[rank] = iso ? dense[0] : dense[i];
+        }
+    }
+}
+
+void gb_bitmap_to_csr(const uint64_t *bits, const void *dense, bool iso, int64_t n, size_t tsize,
+                      int64_t **rowptr, int32_t **colidx, void **vals, int64_t *nvals) {
+    int64_t nw = gb_words(n);
+    int64_t *pop = gb_malloc_n<int64_t>(nw + 1);
+    int64_t *woff = gb_malloc_n<int64_t>(nw + 1);
+    if (nw) {
+        unsigned g = gb_grid(nw);
+        hipLaunchKernelGGL(k_word_pop, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), bits, nw, pop);
+        GB_LAUNCH_CHECK();
+    }
+    gb_exclusive_scan_i64(pop, woff, nw);
+    int64_t nz = gb_read_i64(woff + nw);
+    int64_t *rp = gb_malloc_n<int64_t>(n + 1);
+    int32_t *ci = gb_malloc_n<int32_t>(nz);
+    void *vx = iso ? gb_malloc(tsize) : gb_malloc(nz * tsize);
+    if (iso) gb_copy_d2d(vx, dense, tsize);
+    if (n) {
+        unsigned g = gb_grid(n);
+        if (g > 8192) g = 8192;
+        void *vout = iso ? nullptr : vx;
+        switch (tsize) {
+        case 1: hipLaunchKernelGGL(k_bitmap_scatter<uint8_t>, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), bits, (const uint8_t *)dense, false, n, woff, rp, ci, (uint8_t *)vout); break;
+        case 2: hipLaunchKernelGGL(k_bitmap_scatter<uint16_t>, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), bits, (const uint16_t *)dense, false, n, woff, rp, ci, (uint16_t *)vout); break;
+        case 4: hipLaunchKernelGGL(k_bitmap_scatter<uint32_t>, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), bits, (const uint32_t *)dense, false, n, woff, rp, ci, (uint32_t *)vout); break;
+        default: hipLaunchKernelGGL(k_bitmap_scatter<uint64_t>, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), bits, (const uint64_t *)dense, false, n, woff, rp, ci, (uint64_t *)vout); break;
+        }
+        GB_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(k_copy_i64, dim3(1), dim3(1), 0, gb_stream(), rp + n, woff + nw);
+    GB_LAUNCH_CHECK();
+    gb_free(pop);
+    gb_free(woff);
+    *rowptr = rp;
+    *colidx = ci;
+    *vals = vx;
+    *nvals = nz;
+}
+
+// n x m CSR with m == 1 (or any CSR: entry (i, 0) only) -> bitmap
+template <class W>
+__global__ void k_csr_col_to_bitmap(const int64_t *__restrict__ rowptr, const W *__restrict__ vals,
+                                    bool iso, int64_t n, uint64_t *__restrict__ bits,
+                                    W *__restrict__ dense) {
+    int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    int64_t nw = (n + 63) >> 6;
+    if (w >= nw) return;
+    uint64_t word = 0;
+    for (int b = 0; b < 64; b++) {
+        int64_t i = (w << 6) + b;
+        if (i >= n) break;
+        int64_t p = rowptr[i];
+        if (rowptr[i + 1] > p) {
+            word |= 1ULL << b;
+            if (dense) dense[i] = iso ? vals[0] : vals[p];
+        }
+    }
+    bits[w] = word;
+}
+
+void gb_csr_col_to_bitmap(const gb_csr_view &v, size_t tsize, uint64_t **bits, void **dense,
+                          int64_t **d_nvals) {
+    int64_t n = v.nrows;
+    int64_t nw = gb_words(n);
+    uint64_t *b = gb_malloc_n<uint64_t>(nw);
+    void *d = v.iso ? gb_malloc(tsize) : gb_malloc(n * tsize);
+    if (v.iso) gb_copy_d2d(d, v.vals, tsize);
+    if (nw) {
+        unsigned g = gb_grid(nw);
+        void *dout = v.iso ? nullptr : d;
+        switch (tsize) {
+        case 1: hipLaunchKernelGGL(k_csr_col_to_bitmap<uint8_t>, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), v.rowptr, (const uint8_t *)v.vals, false, n, b, (uint8_t *)dout); break;
+        case 2: hipLaunchKernelGGL(k_csr_col_to_bitmap<uint16_t>, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), v.rowptr, (const uint16_t *)v.vals, false, n, b, (uint16_t *)dout); break;
+        case 4: hipLaunchKernelGGL(k_csr_col_to_bitmap<uint32_t>, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), v.rowptr, (const uint32_t *)v.vals, false, n, b, (uint32_t *)dout); break;
+        default: hipLaunchKernelGGL(k_csr_col_to_bitmap<uint64_t>, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), v.rowptr, (const uint64_t *)v.vals, false, n, b, (uint64_t *)dout); break;
+        }
+        GB_LAUNCH_CHECK();
+    }
+    int64_t *cnt = gb_malloc_n<int64_t>(1);
+    gb_bitmap_count(b, n, cnt);
+    *bits = b;
+    *dense = d;
+    *d_nvals = cnt;
+}
+
+// ------------------------------------------------------------------ transpose
+__global__ void k_expand_rows(const int64_t *__restrict__ rowptr, int64_t nrows,
+                              int64_t *__restrict__ rowof) {
+    // one wave per row
+    int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    int lane = threadIdx.x & 63;
+    int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t i = wave; i < nrows; i += nw)
+        for (int64_t p = rowptr[i] + lane; p < rowptr[i + 1]; p += 64) rowof[p] = i;
+}
+
+__global__ void k_count_cols(const int32_t *__restrict__ colidx, int64_t nvals,
+                             unsigned long long *__restrict__ cnt) {
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < nvals;
+         p += (int64_t)gridDim.x * blockDim.x)
+        atomicAdd(&cnt[colidx[p]], 1ULL);
+}
+
+template <class W>
+__global__ void k_transpose_fill(const int64_t *__restrict__ perm, const int64_t *__restrict__ rowof,
+                                 const W *__restrict__ vals, int64_t nvals,
+                                 int32_t *__restrict__ tcol, W *__restrict__ tvals) {
+    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < nvals;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        int64_t p = perm[q];
+        tcol[q] = (int32_t)rowof[p];
+        if (tvals) tvals[q] = vals[p];
+    }
+}
+
+void gb_transpose_csr(int64_t nrows, int64_t ncols, int64_t nvals, const int64_t *rowptr,
+                      const int32_t *colidx, const void *vals, size_t tsize, bool iso,
+                      int64_t **trowptr, int32_t **tcolidx, void **tvals) {
+    int64_t *trp = gb_malloc_n<int64_t>(ncols + 1);
+    int32_t *tci = gb_malloc_n<int32_t>(nvals);
+    void *tvx = vals ? (iso ? gb_malloc(tsize) : gb_malloc(nvals * tsize)) : nullptr;
+    if (vals && iso) gb_copy_d2d(tvx, vals, tsize);
+    // column counts -> row pointers of the transpose
+    int64_t *cnt = gb_malloc_n<int64_t>(ncols + 1);
+    gb_memset(cnt, 0, (ncols + 1) * sizeof(int64_t));
+    if (nvals) {
+        unsigned g = gb_grid(nvals);
+        if (g > 8192) g = 8192;
+        hipLaunchKernelGGL(k_count_cols, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), colidx, nvals,
+                           (unsigned long long *)cnt);
+        GB_LAUNCH_CHECK();
+    }
+    gb_exclusive_scan_i64(cnt, trp, ncols);
+    gb_free(cnt);
+    if (nvals) {
+        // stable sort of positions by column (rows come out ascending within a column)
+        int32_t *keys = gb_malloc_n<int32_t>(nvals);
+        int64_t *perm = gb_malloc_n<int64_t>(nvals);
+        int64_t *rowof = gb_malloc_n<int64_t>(nvals);
+        gb_copy_d2d(keys, colidx, nvals * sizeof(int32_t));
+        hipLaunchKernelGGL(k_expand_rows, dim3(gb_grid(nrows * 64 > (1LL << 24) ? (1LL << 24) : nrows * 64)),
+                           dim3(GB_BLOCK), 0, gb_stream(), rowptr, nrows, rowof);
+        GB_LAUNCH_CHECK();
+        // perm = 0..nvals-1 : reuse rowof-type iota via thrust-free kernel
+        int64_t *iota = perm;
+        {
+            unsigned g = gb_grid(nvals);
+            if (g > 8192) g = 8192;
+            hipLaunchKernelGGL(k_iota, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), iota, nvals);
+            GB_LAUNCH_CHECK();
+        }
+        int bits = 1;
+        while (bits < 31 && (1LL << bits) < ncols) bits++;
+        gb_sort_pairs_i32(keys, perm, nvals, bits);
+        unsigned g = gb_grid(nvals);
+        if (g > 8192) g = 8192;
+        void *vout = (vals && !iso) ? tvx : nullptr;
+        switch (tsize) {
+        case 1: hipLaunchKernelGGL(k_transpose_fill<uint8_t>, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), perm, rowof, (const uint8_t *)vals, nvals, tci, (uint8_t *)vout); break;
+        case 2: hipLaunchKernelGGL(k_transpose_fill<uint16_t>, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), perm, rowof, (const uint16_t *)vals, nvals, tci, (uint16_t *)vout); break;
+        case 4: hipLaunchKernelGGL(k_transpose_fill<uint32_t>, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), perm, rowof, (const uint32_t *)vals, nvals, tci, (uint32_t *)vout); break;
+        default: hipLaunchKernelGGL(k_transpose_fill<uint64_t>, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), perm, rowof, (const uint64_t *)vals, nvals, tci, (uint64_t *)vout); break;
+        }
+        GB_LAUNCH_CHECK();
+        gb_free(keys);
+        gb_free(perm);
+        gb_free(rowof);
+    }
+    *trowptr = trp;
+    *tcolidx = tci;
+    *tvals = tvx;
+}

@@ -1,0 +1,397 @@
+// gb_writeback.hip -- C<M,replace> = C accum T, the GraphBLAS output rule
+// (C API 2.0 §3.5; SURVEY.md §8(a) rules 2-5) applied after every operation.
+//
+// Most hot-path calls never launch a merge: with no accumulator and either no
+// mask or a mask the kernel already applied under `replace` (BFS:
+// q<!v.S, replace> = ...), T simply becomes C's new storage.  Otherwise a
+// word-parallel (vectors) or row-parallel (matrices) merge runs.
+//
+// Mixed-type accumulators (accum type != C type) are evaluated by casting C
+// and T into the accumulator type, merging there and casting back; entries
+// present only in C therefore make a round trip through the accumulator type.
+#include "gb_dispatch.cuh"
+#include "gb_internal.h"
+
+#define WB_BLOCK 256
+static inline unsigned wb_grid(int64_t n, unsigned cap = 16384) {
+    int64_t g = (n + WB_BLOCK - 1) / WB_BLOCK;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+#define WB_STRIDE(i, n) \
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (n); i += (int64_t)gridDim.x * blockDim.x)
+
+// ================================================================== masks
+template <class T>
+__global__ void k_vmask_values(const uint64_t *__restrict__ bits, const T *__restrict__ vals, bool iso, int64_t n,
+                               uint64_t *__restrict__ out) {
+    WB_STRIDE(w, (n + 63) >> 6) {
+        uint64_t word = bits[w], r = 0;
+        while (word) {
+            int b = __ffsll((unsigned long long)word) - 1;
+            word &= word - 1;
+            int64_t i = (w << 6) + b;
+            if (gb_cast<bool, T>(iso ? vals[0] : vals[i])) r |= 1ULL << b;
+        }
+        out[w] = r;
+    }
+}
+
+void gb_make_vmask(gb_vmask &m, GB_Obj *M, const gb_desc &d, int64_t n) {
+    m.comp = d.comp;
+    if (!M) {
+        if (d.comp) {  // ~NULL: nothing is selected
+            uint64_t *z = m.own.get<uint64_t>(gb_words(n));
+            gb_memset(z, 0, gb_words(n) * sizeof(uint64_t));
+            m.bits = z;
+            m.comp = false;
+        }
+        return;
+    }
+    GB_REQUIRE(M->nrows == n && (M->kind != GB_KIND_MATRIX || M->ncols == 1), GrB_DIMENSION_MISMATCH,
+               "mask dimensions do not match the output");
+    gb_bitmap_view *bv = new gb_bitmap_view();  // owned by m.own through a small holder below
+    gb_get_bitmap(*bv, M);
+    if (d.structure) {
+        // copy only when the view owns temporaries (matrix-typed mask)
+        if (bv->own.n) {
+            uint64_t *c = m.own.get<uint64_t>(gb_words(n));
+            gb_copy_d2d(c, bv->bits, gb_words(n) * sizeof(uint64_t));
+            m.bits = c;
+        } else {
+            m.bits = bv->bits;
+        }
+    } else {
+        uint64_t *c = m.own.get<uint64_t>(gb_words(n));
+        gb_with_type(bv->tcode, [&](auto z) {
+            using T = decltype(z);
+            hipLaunchKernelGGL(k_vmask_values<T>, dim3(wb_grid(gb_words(n))), dim3(WB_BLOCK), 0, gb_stream(), bv->bits,
+                               (const T *)bv->vals, bv->iso, n, c);
+        });
+        GB_LAUNCH_CHECK();
+        m.bits = c;
+    }
+    delete bv;  // stream-ordered frees of its temporaries happen after the copies above
+}
+
+template <class T>
+__global__ void k_mmask_count(const int64_t *__restrict__ rp, const T *__restrict__ vals, bool iso, int64_t nrows,
+                              int64_t *__restrict__ cnt) {
+    WB_STRIDE(i, nrows) {
+        int64_t c = 0;
+        for (int64_t p = rp[i]; p < rp[i + 1]; p++) c += gb_cast<bool, T>(iso ? vals[0] : vals[p]);
+        cnt[i] = c;
+    }
+}
+template <class T>
+__global__ void k_mmask_fill(const int64_t *__restrict__ rp, const int32_t *__restrict__ ci, const T *__restrict__ vals,
+                             bool iso, int64_t nrows, const int64_t *__restrict__ rp2, int32_t *__restrict__ ci2) {
+    WB_STRIDE(i, nrows) {
+        int64_t o = rp2[i];
+        for (int64_t p = rp[i]; p < rp[i + 1]; p++)
+            if (gb_cast<bool, T>(iso ? vals[0] : vals[p])) ci2[o++] = ci[p];
+    }
+}
+
+void gb_make_mmask(gb_mmask &m, GB_Obj *M, const gb_desc &d, int64_t nrows, int64_t ncols) {
+    m.comp = d.comp;
+    if (!M) {
+        if (d.comp) {  // ~NULL: an empty structure, not complemented = nothing selected
+            m.present = true;
+            m.comp = false;
+            int64_t *rp = m.own.get<int64_t>(nrows + 1);
+            gb_memset(rp, 0, (nrows + 1) * sizeof(int64_t));
+            m.rowptr = rp;
+            m.colidx = m.own.get<int32_t>(1);
+            m.nvals = 0;
+        }
+        return;
+    }
+    int64_t mcols = M->kind == GB_KIND_MATRIX ? M->ncols : 1;
+    GB_REQUIRE(M->nrows == nrows && mcols == ncols, GrB_DIMENSION_MISMATCH, "mask dimensions do not match the output");
+    m.present = true;
+    gb_get_csr(m.view, M);
+    if (d.structure) {
+        m.rowptr = m.view.rowptr;
+        m.colidx = m.view.colidx;
+        m.nvals = m.view.nvals;
+        return;
+    }
+    int64_t *cnt = m.own.get<int64_t>(nrows + 1);
+    int64_t *rp2 = m.own.get<int64_t>(nrows + 1);
+    gb_memset(cnt, 0, (nrows + 1) * sizeof(int64_t));
+    gb_with_type(m.view.tcode, [&](auto z) {
+        using T = decltype(z);
+        if (nrows)
+            hipLaunchKernelGGL(k_mmask_count<T>, dim3(wb_grid(nrows)), dim3(WB_BLOCK), 0, gb_stream(), m.view.rowptr,
+                               (const T *)m.view.vals, m.view.iso, nrows, cnt);
+    });
+    GB_LAUNCH_CHECK();
+    gb_exclusive_scan_i64(cnt, rp2, nrows);
+    int64_t nz = gb_read_i64(rp2 + nrows);
+    int32_t *ci2 = m.own.get<int32_t>(nz);
+    gb_with_type(m.view.tcode, [&](auto z) {
+        using T = decltype(z);
+        if (nrows)
+            hipLaunchKernelGGL(k_mmask_fill<T>, dim3(wb_grid(nrows)), dim3(WB_BLOCK), 0, gb_stream(), m.view.rowptr,
+                               m.view.colidx, (const T *)m.view.vals, m.view.iso, nrows, rp2, ci2);
+    });
+    GB_LAUNCH_CHECK();
+    m.rowptr = rp2;
+    m.colidx = ci2;
+    m.nvals = nz;
+}
+
+// ================================================================== vectors
+template <class CT>
+__global__ __launch_bounds__(WB_BLOCK) void k_vec_merge(
+    int64_t n, const uint64_t *__restrict__ cbits, const CT *__restrict__ cvals, bool c_iso,
+    const uint64_t *__restrict__ tbits, const CT *__restrict__ tvals, bool t_iso, const uint64_t *__restrict__ mbits,
+    bool mcomp, bool replace, int accum, uint64_t *__restrict__ obits, CT *__restrict__ ovals,
+    unsigned long long *__restrict__ count) {
+    unsigned long long mine = 0;
+    // 64 consecutive elements per wave -> one output word per wave
+    for (int64_t base = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) & ~63LL; base < n;
+         base += (int64_t)gridDim.x * blockDim.x) {
+        int64_t i = base + (threadIdx.x & 63);
+        bool inr = i < n;
+        bool c = inr && gb_bit(cbits, i);
+        bool t = inr && gb_bit(tbits, i);
+        bool m = inr && (mbits ? (gb_bit(mbits, i) != mcomp) : !mcomp);
+        bool have = false;
+        CT v = CT();
+        if (m) {
+            if (accum >= 0 && c && t) {
+                v = gb_binop<CT>(accum, cvals[c_iso ? 0 : i], tvals[t_iso ? 0 : i]);
+                have = true;
+            } else if (t) {
+                v = tvals[t_iso ? 0 : i];
+                have = true;
+            } else if (accum >= 0 && c) {
+                v = cvals[c_iso ? 0 : i];
+                have = true;
+            }
+        } else if (!replace && c) {
+            v = cvals[c_iso ? 0 : i];
+            have = true;
+        }
+        if (have) ovals[i] = v;
+        unsigned long long word = __ballot(have);
+        if ((threadIdx.x & 63) == 0) {
+            obits[base >> 6] = word;
+            mine += __popcll(word);
+        }
+    }
+    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(count, mine);
+}
+
+static void cast_vec_result(gb_vec_result &T, int code) {
+    if (T.tcode == code) return;
+    int64_t nv = T.iso ? 1 : T.n;
+    void *d = gb_malloc(nv * gb_type_size(code));
+    gb_cast_array(d, code, T.dense, T.tcode, nv);
+    gb_free(T.dense);
+    T.dense = d;
+    T.tcode = code;
+}
+
+static void free_vec_result(gb_vec_result &T) {
+    gb_free(T.bits);
+    gb_free(T.dense);
+    gb_free(T.d_nvals);
+    T.bits = nullptr;
+    T.dense = nullptr;
+    T.d_nvals = nullptr;
+}
+
+void gb_writeback_vector(GB_Obj *C, gb_vec_result &T, GB_Obj *M, const gb_desc &d, GrB_BinaryOp accum,
+                         bool t_within_mask) {
+    const int ct = C->type->code;
+    const int64_t n = T.n;
+    GB_REQUIRE(C->nrows == n, GrB_DIMENSION_MISMATCH, "output size mismatch");
+    bool no_mask = (M == nullptr && !d.comp);
+    if (!accum && (no_mask || (t_within_mask && d.replace))) {
+        cast_vec_result(T, ct);
+        gb_install_bitmap(C, n, T.bits, T.dense, T.iso, T.d_nvals);
+        T.bits = nullptr;
+        T.dense = nullptr;
+        T.d_nvals = nullptr;
+        return;
+    }
+    // general merge
+    int wcode = ct;
+    if (accum) {
+        GB_REQUIRE(accum->magic == GB_MAGIC, GrB_UNINITIALIZED_OBJECT, "invalid accum");
+        GB_REQUIRE(accum->xtype != nullptr, GrB_DOMAIN_MISMATCH, "positional accumulator");
+        wcode = accum->xtype->code;
+    }
+    gb_vmask mask;
+    gb_make_vmask(mask, M, d, n);
+    gb_bitmap_view cv;
+    gb_get_bitmap(cv, C);
+    gb_scratch s;
+    const void *cvals = cv.vals;
+    bool c_iso = cv.iso;
+    if (wcode != ct) {
+        cvals = gb_bitmap_vals_as(cv, wcode, s);
+    }
+    cast_vec_result(T, wcode);
+    uint64_t *obits = gb_malloc_n<uint64_t>(gb_words(n));
+    void *ovals = gb_malloc(n * gb_type_size(wcode));
+    int64_t *cnt = gb_malloc_n<int64_t>(1);
+    gb_memset(cnt, 0, sizeof(int64_t));
+    if (n) {
+        gb_with_type(wcode, [&](auto z) {
+            using W = decltype(z);
+            hipLaunchKernelGGL(k_vec_merge<W>, dim3(wb_grid(n)), dim3(WB_BLOCK), 0, gb_stream(), n, cv.bits,
+                               (const W *)cvals, c_iso, T.bits, (const W *)T.dense, T.iso, mask.bits, mask.comp,
+                               d.replace, accum ? accum->opcode : -1, obits, (W *)ovals,
+                               (unsigned long long *)cnt);
+        });
+        GB_LAUNCH_CHECK();
+    }
+    free_vec_result(T);
+    if (wcode != ct) {
+        void *o2 = gb_malloc(n * gb_type_size(ct));
+        gb_cast_array(o2, ct, ovals, wcode, n);
+        gb_free(ovals);
+        ovals = o2;
+    }
+    gb_install_bitmap(C, n, obits, ovals, false, cnt);
+}
+
+// ================================================================== matrices
+template <class CT, bool FILL>
+__global__ __launch_bounds__(WB_BLOCK) void k_mat_merge(
+    int64_t nrows, const int64_t *__restrict__ crp, const int32_t *__restrict__ cci, const CT *__restrict__ cvx,
+    bool c_iso, const int64_t *__restrict__ trp, const int32_t *__restrict__ tci, const CT *__restrict__ tvx,
+    bool t_iso, const int64_t *__restrict__ mrp, const int32_t *__restrict__ mci, bool has_mask, bool mcomp,
+    bool replace, int accum, int64_t *__restrict__ orp, int32_t *__restrict__ oci, CT *__restrict__ ovx) {
+    WB_STRIDE(i, nrows) {
+        int64_t pc = crp[i], ec = crp[i + 1], pt = trp[i], et = trp[i + 1];
+        int64_t pm = has_mask ? mrp[i] : 0, em = has_mask ? mrp[i + 1] : 0;
+        int64_t o = FILL ? orp[i] : 0;
+        while (pc < ec || pt < et) {
+            int32_t jc = pc < ec ? cci[pc] : INT32_MAX;
+            int32_t jt = pt < et ? tci[pt] : INT32_MAX;
+            int32_t j = jc < jt ? jc : jt;
+            bool c = jc == j, t = jt == j;
+            bool m;
+            if (has_mask) {
+                while (pm < em && mci[pm] < j) pm++;
+                m = (pm < em && mci[pm] == j) != mcomp;
+            } else {
+                m = !mcomp;
+            }
+            bool have = false;
+            CT v = CT();
+            if (m) {
+                if (accum >= 0 && c && t) {
+                    if (FILL) v = gb_binop<CT>(accum, cvx[c_iso ? 0 : pc], tvx[t_iso ? 0 : pt]);
+                    have = true;
+                } else if (t) {
+                    if (FILL) v = tvx[t_iso ? 0 : pt];
+                    have = true;
+                } else if (accum >= 0 && c) {
+                    if (FILL) v = cvx[c_iso ? 0 : pc];
+                    have = true;
+                }
+            } else if (!replace && c) {
+                if (FILL) v = cvx[c_iso ? 0 : pc];
+                have = true;
+            }
+            if (have) {
+                if (FILL) {
+                    oci[o] = j;
+                    ovx[o] = v;
+                }
+                o++;
+            }
+            if (c) pc++;
+            if (t) pt++;
+        }
+        if (!FILL) orp[i] = o;
+    }
+}
+
+static void cast_mat_result(gb_mat_result &T, int code) {
+    if (T.tcode == code) return;
+    int64_t nv = T.iso ? 1 : T.nvals;
+    void *d = gb_malloc(nv * gb_type_size(code));
+    gb_cast_array(d, code, T.vals, T.tcode, nv);
+    gb_free(T.vals);
+    T.vals = d;
+    T.tcode = code;
+}
+
+void gb_writeback_matrix(GB_Obj *C, gb_mat_result &T, GB_Obj *M, const gb_desc &d, GrB_BinaryOp accum) {
+    const int ct = C->type->code;
+    const int64_t nrows = T.nrows, ncols = T.ncols;
+    int64_t cncols = C->kind == GB_KIND_MATRIX ? C->ncols : 1;
+    GB_REQUIRE(C->nrows == nrows && cncols == ncols, GrB_DIMENSION_MISMATCH, "output dimensions mismatch");
+    bool no_mask = (M == nullptr && !d.comp);
+    int64_t cnv = gb_nvals(C);
+    bool fast = false;
+    if (no_mask && (!accum || cnv == 0)) fast = true;                  // C = T  (or C empty: C = T)
+    if (T.within_mask && !d.comp && M && (d.replace || cnv == 0) && (!accum || cnv == 0)) fast = true;
+    if (fast) {
+        cast_mat_result(T, ct);
+        gb_install_csr(C, nrows, ncols, T.nvals, T.rowptr, T.colidx, T.vals, T.iso);
+        T.rowptr = nullptr;
+        T.colidx = nullptr;
+        T.vals = nullptr;
+        return;
+    }
+    int wcode = ct;
+    if (accum) {
+        GB_REQUIRE(accum->magic == GB_MAGIC, GrB_UNINITIALIZED_OBJECT, "invalid accum");
+        GB_REQUIRE(accum->xtype != nullptr, GrB_DOMAIN_MISMATCH, "positional accumulator");
+        wcode = accum->xtype->code;
+    }
+    gb_mmask mask;
+    gb_make_mmask(mask, M, d, nrows, ncols);
+    gb_csr_view cv;
+    gb_get_csr(cv, C);
+    gb_scratch s;
+    const void *cvals = (wcode != ct) ? gb_view_vals_as(cv, wcode, s) : cv.vals;
+    cast_mat_result(T, wcode);
+    int64_t *cnt = s.get<int64_t>(nrows + 1);
+    int64_t *orp = gb_malloc_n<int64_t>(nrows + 1);
+    bool has_mask = mask.present;
+    gb_with_type(wcode, [&](auto z) {
+        using W = decltype(z);
+        if (nrows)
+            hipLaunchKernelGGL((k_mat_merge<W, false>), dim3(wb_grid(nrows)), dim3(WB_BLOCK), 0, gb_stream(), nrows,
+                               cv.rowptr, cv.colidx, (const W *)cvals, cv.iso, T.rowptr, T.colidx, (const W *)T.vals,
+                               T.iso, mask.rowptr, mask.colidx, has_mask, mask.comp, d.replace,
+                               accum ? accum->opcode : -1, cnt, nullptr, nullptr);
+    });
+    GB_LAUNCH_CHECK();
+    gb_exclusive_scan_i64(cnt, orp, nrows);
+    int64_t nz = gb_read_i64(orp + nrows);
+    int32_t *oci = gb_malloc_n<int32_t>(nz);
+    void *ovx = gb_malloc(nz * gb_type_size(wcode));
+    gb_with_type(wcode, [&](auto z) {
+        using W = decltype(z);
+        if (nrows)
+            hipLaunchKernelGGL((k_mat_merge<W, true>), dim3(wb_grid(nrows)), dim3(WB_BLOCK), 0, gb_stream(), nrows,
+                               cv.rowptr, cv.colidx, (const W *)cvals, cv.iso, T.rowptr, T.colidx, (const W *)T.vals,
+                               T.iso, mask.rowptr, mask.colidx, has_mask, mask.comp, d.replace,
+                               accum ? accum->opcode : -1, orp, oci, (W *)ovx);
+    });
+    GB_LAUNCH_CHECK();
+    gb_free(T.rowptr);
+    gb_free(T.colidx);
+    gb_free(T.vals);
+    T.rowptr = nullptr;
+    T.colidx = nullptr;
+    T.vals = nullptr;
+    if (wcode != ct) {
+        void *o2 = gb_malloc(nz * gb_type_size(ct));
+        gb_cast_array(o2, ct, ovx, wcode, nz);
+        gb_free(ovx);
+        ovx = o2;
+    }
+    gb_install_csr(C, nrows, ncols, nz, orp, oci, ovx, false);
+}

@@ -1,0 +1,60 @@
+"""`A @ B` delayed matmul expressions (reference core/infix.py:251-259, 388-397,
+444-497; default semiring resolution core/expr.py:504-508)."""
+from . import operator as _op
+
+
+class InfixExpr:
+    def __init__(self, left, right, method):
+        self.left = left
+        self.right = right
+        self.method = method
+
+    def _with_op(self, op):
+        return getattr(self.left, self.method)(self.right, op)
+
+    def _to_expr(self):
+        return self._with_op(_op.semiring.plus_times)
+
+    def new(self, dtype=None, *, mask=None, name=None, **opts):
+        return self._to_expr().new(dtype, mask=mask, name=name, **opts)
+
+    @property
+    def dtype(self):
+        return self._to_expr().dtype
+
+    @property
+    def size(self):
+        return self._to_expr().size
+
+    @property
+    def nrows(self):
+        return self._to_expr().nrows
+
+    @property
+    def ncols(self):
+        return self._to_expr().ncols
+
+    @property
+    def shape(self):
+        return self._to_expr().shape
+
+
+def _matmul_infix_expr(left, right):
+    from .matrix import Matrix, TransposedMatrix
+    from .vector import Vector
+
+    lm = isinstance(left, (Matrix, TransposedMatrix))
+    rm = isinstance(right, (Matrix, TransposedMatrix))
+    if lm and rm:
+        method = "mxm"
+    elif lm and isinstance(right, Vector):
+        method = "mxv"
+    elif isinstance(left, Vector) and rm:
+        method = "vxm"
+    elif isinstance(left, Vector) and isinstance(right, Vector):
+        method = "inner"
+    else:
+        return NotImplemented
+    expr = InfixExpr(left, right, method)
+    expr._to_expr()  # shape check now (reference core/infix.py:492)
+    return expr

@@ -658,3 +658,52 @@ int or_bfs_levels(const or_csr *A, int64_t src, int32_t *levels, int64_t *edges)
     if (edges) *edges = e;
     return lev;
 }
+
+/* Level BFS exactly as the reference notebook loop (Example B.1 cell 8), every
+ * step through or_mxm:  v[:](mask=q.V) << d ; q(~v.S, replace) << q.vxm(A, lor_land).
+ * This is the CPU baseline "port" of the GraphBLAS formulation. */
+int or_bfs_graphblas(const or_csr *A, int64_t src, int32_t *levels, int64_t *edges) {
+    int64_t n = A->nrows;
+    memset(levels, 0, (size_t)n * sizeof(int32_t));
+    /* q: 1 x n BOOL row */
+    or_csr q = {1, n, GBAMD_T_BOOL, NULL, NULL, NULL};
+    q.p = (int64_t *)xmalloc(2 * sizeof(int64_t));
+    q.j = (int64_t *)xmalloc(sizeof(int64_t));
+    q.x = xmalloc(1);
+    q.p[0] = 0; q.p[1] = 1; q.j[0] = src; ((uint8_t *)q.x)[0] = 1;
+    /* v: visited structure as a 1 x n row (values unused: structural mask) */
+    or_csr v = {1, n, GBAMD_T_INT32, NULL, NULL, NULL};
+    v.p = (int64_t *)calloc(2, sizeof(int64_t));
+    v.j = (int64_t *)xmalloc((size_t)n * sizeof(int64_t));
+    v.x = NULL;
+    int d = 0;
+    int64_t e = 0;
+    for (;;) {
+        d++;
+        /* v<q.V> = d : merge q's true entries into the sorted visited list */
+        int64_t nv = v.p[1], nq = q.p[1], a = 0, b = 0, o = 0;
+        int64_t *nj = (int64_t *)xmalloc((size_t)(nv + nq + 1) * sizeof(int64_t));
+        while (a < nv || b < nq) {
+            int64_t ja = a < nv ? v.j[a] : INT64_MAX;
+            int64_t jb = INT64_MAX;
+            while (b < nq && !((uint8_t *)q.x)[b]) b++;
+            if (b < nq) jb = q.j[b];
+            if (ja == INT64_MAX && jb == INT64_MAX) break;
+            if (jb < ja) { nj[o++] = jb; levels[jb] = d; e += A->p[jb + 1] - A->p[jb]; b++; }
+            else if (ja < jb) { nj[o++] = ja; a++; }
+            else { nj[o++] = ja; a++; b++; }
+        }
+        free(v.j); v.j = nj; v.p[1] = o;
+        /* q(~v.S, replace) << q.vxm(A, lor_land) */
+        or_csr q0 = q;
+        or_mxm(&q, &v, 1, 1, 1, -1, 0, 0, GBAMD_MON_LOR, GBAMD_OP_LAND, GBAMD_T_BOOL, GBAMD_T_BOOL,
+               &q0, 0, A, 0);
+        or_csr_free(&q0);
+        int any = 0;
+        for (int64_t t = 0; t < q.p[1]; t++) if (((uint8_t *)q.x)[t]) { any = 1; break; }
+        if (!any) break;
+    }
+    or_csr_free(&q); or_csr_free(&v);
+    if (edges) *edges = e;
+    return d;
+}
