@@ -28,7 +28,10 @@ GB_HD T gb_tmax() {
     if constexpr (std::is_same<T, bool>::value) return true;
     else if constexpr (std::is_same<T, float>::value) return __builtin_inff();
     else if constexpr (std::is_same<T, double>::value) return __builtin_inf();
-    else if constexpr (std::is_signed<T>::value) return (T)(~(typename std::make_unsigned<T>::type)0 >> 1);
+    else if constexpr (std::is_signed<T>::value) {
+        using U = typename std::make_unsigned<T>::type;
+        return (T)(U)((U)~U(0) >> 1);  // cast before the shift: narrow types promote to int
+    }
     else return (T)~(T)0;
 }
 template <class T>

@@ -232,6 +232,7 @@ gb_desc gb_read_desc(const GrB_Descriptor d);
 struct gb_vmask {
     const uint64_t *bits = nullptr;  // nullptr: no mask
     bool comp = false;
+    const int64_t *count = nullptr;  // device count of set mask bits, when known
     gb_scratch own;
 };
 void gb_make_vmask(gb_vmask &m, GB_Obj *M, const gb_desc &d, int64_t n);
@@ -272,8 +273,11 @@ void gb_writeback_matrix(GB_Obj *C, gb_mat_result &T, GB_Obj *M, const gb_desc &
                          GrB_BinaryOp accum);
 
 // kernels of the hot path (gb_mxv.hip, gb_mxm.hip)
-void gb_spmv(gb_vec_result &T, const gb_csr_view &A, gb_bitmap_view &u, const gb_vmask &mask,
-             GrB_Semiring sr, bool flip);
+// A: rows = output positions (pull); Apush: the other orientation (rows = u's
+// positions) or nullptr; the device picks push or pull per call.
+void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, gb_bitmap_view &u,
+             const gb_vmask &mask, GrB_Semiring sr, bool flip);
+bool gb_spmv_result_iso(GrB_Semiring sr, bool a_iso, bool u_iso, bool flip);
 void gb_spgemm(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, gb_csr_view *BT,
                gb_mmask &mask, GrB_Semiring sr);
 

@@ -60,7 +60,7 @@ __global__ __launch_bounds__(MXM_BLOCK) void k_dot_masked(
                 pb++;
             } else {
                 X a = X(), b = X();
-                if (SR::reads_values) {
+                if (SR::reads_values && avx && bvx) {
                     a = avx[a_iso ? 0 : pa];
                     b = bvx[b_iso ? 0 : pb];
                 }
@@ -135,12 +135,13 @@ __global__ __launch_bounds__(MXM_BLOCK) void k_expand(
         int64_t i = rowof[q];
         int32_t k = aci[p];
         X a = X();
-        if (SR::reads_values) a = avx[a_iso ? 0 : p];
+        const bool rv = SR::reads_values && avx && bvx;
+        if (rv) a = avx[a_iso ? 0 : p];
         int64_t base = eoff[q], b0 = brp[k], b1 = brp[k + 1];
         for (int64_t pb = b0 + lane; pb < b1; pb += 64) {
             int32_t j = bci[pb];
             X b = X();
-            if (SR::reads_values) b = bvx[b_iso ? 0 : pb];
+            if (rv) b = bvx[b_iso ? 0 : pb];
             int64_t o = base + (pb - b0);
             keys[o] = ((uint64_t)(i - r0) << 32) | (uint32_t)j;
             perm[o] = o;

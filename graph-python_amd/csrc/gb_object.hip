@@ -1342,6 +1342,38 @@ GrB_Info GxB_Vector_device_touch(GrB_Vector v) {
         o->nvals_valid = false;
     });
 }
+GrB_Info GxB_Vector_bitmap_export(GrB_Vector v, void *dst, GrB_Index nwords) {
+    return gb_api(OBJ(v), [&] {
+        GB_Obj *o = gb_obj_check(v);
+        GB_REQUIRE(o->kind != GB_KIND_MATRIX, GrB_INVALID_OBJECT, "not a vector");
+        GB_REQUIRE((int64_t)nwords <= gb_words(o->nrows), GrB_INVALID_VALUE, "too many words");
+        gb_copy_d2d(dst, o->bits, nwords * sizeof(uint64_t));
+    });
+}
+GrB_Info GxB_Vector_bitmap_import(GrB_Vector v, const void *src, GrB_Index nwords) {
+    return gb_api(OBJ(v), [&] {
+        GB_Obj *o = gb_obj_check(v);
+        GB_REQUIRE(o->kind != GB_KIND_MATRIX, GrB_INVALID_OBJECT, "not a vector");
+        GB_REQUIRE((int64_t)nwords == gb_words(o->nrows), GrB_INVALID_VALUE, "word count mismatch");
+        gb_copy_d2d(o->bits, src, nwords * sizeof(uint64_t));
+        // every imported entry carries the value 1 (true): an iso vector
+        size_t ts = o->type->size;
+        char one[16] = {0};
+        with_type(o->type->code, [&](auto z) {
+            using T = decltype(z);
+            T x = (T)1;
+            memcpy(one, &x, sizeof(T));
+        });
+        if (!o->dense || !o->iso) {
+            gb_free(o->dense);
+            o->dense = gb_malloc(ts);
+        }
+        gb_copy_h2d(o->dense, one, ts);
+        o->iso = true;
+        gb_bitmap_count(o->bits, o->nrows, o->d_nvals);
+        o->nvals_valid = false;
+    });
+}
 GrB_Info GxB_Matrix_prepare_transpose(GrB_Matrix A) {
     return gb_api(OBJ(A), [&] {
         GB_Obj *o = gb_obj_check(A);

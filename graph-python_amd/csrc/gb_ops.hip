@@ -47,15 +47,23 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
     int64_t a_cols = (vxm ? (d.tran1 ? ncols_of(A) : A->nrows) : (d.tran0 ? A->nrows : ncols_of(A)));
     GB_REQUIRE(u->nrows == a_cols && ncols_of(u) == 1, GrB_DIMENSION_MISMATCH, "u size does not match A");
     GB_REQUIRE(w->nrows == a_rows && ncols_of(w) == 1, GrB_DIMENSION_MISMATCH, "w size does not match A");
-    gb_csr_view av;
+    gb_csr_view av, pv;
     if (use_csc) gb_get_csc(av, A);
     else gb_get_csr(av, A);
     gb_bitmap_view uv;
     gb_get_bitmap(uv, u);
     gb_vmask m;
     gb_make_vmask(m, mask, d, a_rows);
+    // the other orientation (cached on matrices) enables the push direction for iso results
+    const gb_csr_view *push = nullptr;
+    if (A->kind == GB_KIND_MATRIX && gb_knob("spmv_direction") != 1 &&
+        gb_spmv_result_iso(sr, A->iso, uv.iso, vxm)) {
+        if (use_csc) gb_get_csr(pv, A);
+        else gb_get_csc(pv, A);
+        push = &pv;
+    }
     gb_vec_result T;
-    gb_spmv(T, av, uv, m, sr, vxm);
+    gb_spmv(T, av, push, uv, m, sr, vxm);
     gb_writeback_vector(w, T, mask, d, accum, true);
 }
 
@@ -401,6 +409,89 @@ static GrB_BinaryOp second_of(int code) {
     return (GrB_BinaryOp)h;
 }
 
+// w<M, replace>(:) = x with no accumulator, in place: one pass over the bitmap,
+// values written only where the mask selects (BFS level stamping,
+// notebooks/Example B.1 cell 8: v[:](mask=q.V) << d).  Waves whose 64 mask bits
+// select nothing (and do not replace) leave their word untouched.
+template <class T>
+__global__ __launch_bounds__(OPS_BLOCK) void k_assign_all_scalar(
+    int64_t n, uint64_t *__restrict__ cbits, T *__restrict__ cvals, const uint64_t *__restrict__ mbits, bool mcomp,
+    bool replace, T x, unsigned long long *__restrict__ count) {
+    unsigned long long mine = 0;
+    for (int64_t base = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) & ~63LL; base < n;
+         base += (int64_t)gridDim.x * blockDim.x) {
+        const int lane = threadIdx.x & 63;
+        const int64_t w = base >> 6;
+        const int64_t i = base + lane;
+        uint64_t mword = mbits ? mbits[w] : 0;
+        if (mbits && !mcomp && mword == 0 && !replace) {
+            if (lane == 0) mine += __popcll(cbits[w]);
+            continue;
+        }
+        const uint64_t cword = cbits[w];
+        bool inr = i < n;
+        bool m = inr && (mbits ? ((((mword >> lane) & 1ULL) != 0) != mcomp) : !mcomp);
+        bool c = (cword >> lane) & 1ULL;
+        if (m) cvals[i] = x;
+        bool have = m || (!replace && c && inr);
+        unsigned long long word = __ballot(have);
+        if (lane == 0) {
+            cbits[w] = word;
+            mine += __popcll(word);
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) mine += __shfl_xor(mine, off, 64);
+    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(count, mine);
+}
+
+static bool assign_all_scalar_fast(GB_Obj *w, GB_Obj *mask, const char *xc, const gb_desc &d) {
+    if (w->kind == GB_KIND_MATRIX) return false;
+    const int64_t n = w->nrows;
+    const size_t ts = w->type->size;
+    gb_vmask m;
+    gb_make_vmask(m, mask, d, n);
+    if (!m.bits && !m.comp) {
+        // no mask: w becomes full and iso x
+        int64_t nw = gb_words(n);
+        uint64_t *bits = gb_malloc_n<uint64_t>(nw);
+        gb_memset(bits, 0xff, nw * sizeof(uint64_t));
+        if (n & 63) {
+            uint64_t last = (1ULL << (n & 63)) - 1;
+            gb_copy_h2d(bits + nw - 1, &last, sizeof(last));
+        }
+        void *dense = gb_malloc(ts);
+        gb_copy_h2d(dense, xc, ts);
+        int64_t *cnt = gb_malloc_n<int64_t>(1);
+        gb_copy_h2d(cnt, &n, sizeof(int64_t));
+        gb_sync();  // the host-side sources above live on this stack frame
+        gb_install_bitmap(w, n, bits, dense, true, cnt);
+        return true;
+    }
+    // make the value array writable (non-iso, allocated)
+    if (!w->dense) {
+        w->dense = gb_malloc(n * ts);
+        w->iso = false;
+    } else if (w->iso) {
+        void *full = gb_expand_iso(w->dense, ts, n);
+        gb_free(w->dense);
+        w->dense = full;
+        w->iso = false;
+    }
+    gb_memset(w->d_nvals, 0, sizeof(int64_t));
+    unsigned grid = (unsigned)std::min<int64_t>((n + OPS_BLOCK - 1) / OPS_BLOCK, 8192);
+    gb_with_type(w->type->code, [&](auto z) {
+        using T = decltype(z);
+        T xv;
+        memcpy(&xv, xc, sizeof(T));
+        if (n)
+            hipLaunchKernelGGL(k_assign_all_scalar<T>, dim3(grid), dim3(OPS_BLOCK), 0, gb_stream(), n, w->bits,
+                               (T *)w->dense, m.bits, m.comp, d.replace, xv, (unsigned long long *)w->d_nvals);
+    });
+    GB_LAUNCH_CHECK();
+    w->nvals_valid = false;
+    return true;
+}
+
 static void vector_assign_scalar(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, const void *x, int xcode,
                                  const GrB_Index *I, int64_t ni, const gb_desc &d) {
     check_binop(accum, true);
@@ -418,6 +509,7 @@ static void vector_assign_scalar(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, co
             memcpy(xc, &dv, sizeof(D));
         });
     });
+    if (I == GrB_ALL && !accum && assign_all_scalar_fast(w, mask, xc, d)) return;
     gb_vec_result T;
     scalar_vec_T(T, w->nrows, I, ni, xc, ct);
     GrB_BinaryOp acc = accum;

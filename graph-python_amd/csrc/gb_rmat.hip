@@ -33,7 +33,8 @@ GB_HD uint64_t rm_scramble(uint64_t v, int scale, uint64_t k1, uint64_t k2) {
 }
 
 __global__ void k_rmat_edges(int64_t ne, int scale, uint64_t s0, uint64_t k1, uint64_t k2, uint64_t rb,
-                             uint64_t re, uint64_t *__restrict__ keys, unsigned long long *__restrict__ count) {
+                             uint64_t re, bool transpose, uint64_t *__restrict__ keys,
+                             unsigned long long *__restrict__ count) {
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
         uint64_t r = 0, c = 0;
         for (int l = 0; l < scale; l++) {
@@ -44,6 +45,11 @@ __global__ void k_rmat_edges(int64_t ne, int scale, uint64_t s0, uint64_t k1, ui
         }
         r = rm_scramble(r, scale, k1, k2);
         c = rm_scramble(c, scale, k1, k2);
+        if (transpose) {  // generate rows of A^T: swap the endpoints
+            uint64_t t = r;
+            r = c;
+            c = t;
+        }
         bool keep = (r != c) && r >= rb && r < re;
         // keys outside the shard / self-loops sort to the end and are dropped
         keys[e] = keep ? (((r - rb) << 32) | c) : ~0ULL;
@@ -66,13 +72,19 @@ __global__ void k_rmat_emit(const uint64_t *__restrict__ k, const int64_t *__res
 }
 
 __global__ void k_rmat_values(const int64_t *__restrict__ rowptr, const int32_t *__restrict__ colidx, int64_t nrows,
-                              int64_t rb, uint64_t s0, int kind, void *__restrict__ vals) {
+                              int64_t rb, uint64_t s0, int kind, bool transpose, void *__restrict__ vals) {
     int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     int lane = threadIdx.x & 63;
     int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
     for (int64_t i = wave; i < nrows; i += nw)
         for (int64_t p = rowptr[i] + lane; p < rowptr[i + 1]; p += 64) {
-            uint64_t h = rm_smix(s0 ^ (((uint64_t)(i + rb) << 32) | (uint64_t)(uint32_t)colidx[p]));
+            uint64_t gi = (uint64_t)(i + rb), gj = (uint64_t)(uint32_t)colidx[p];
+            if (transpose) {
+                uint64_t t = gi;
+                gi = gj;
+                gj = t;
+            }
+            uint64_t h = rm_smix(s0 ^ ((gi << 32) | gj));
             if (kind == 1) ((int64_t *)vals)[p] = 1 + (int64_t)(h % 255);
             else ((double *)vals)[p] = (double)(h >> 11) * 0x1.0p-53;
         }
@@ -88,6 +100,8 @@ extern "C" GrB_Info GxB_Matrix_rmat(GrB_Matrix *A, int scale, int edge_factor, u
         if (row_end == 0 || (int64_t)row_end > n) row_end = n;
         GB_REQUIRE(row_begin < row_end, GrB_INVALID_VALUE, "empty row range");
         const int64_t nr = (int64_t)(row_end - row_begin);
+        const bool transpose = (values & 0x100) != 0;
+        values &= 0xff;
         GrB_Type t = values == 1 ? GrB_INT64 : values == 2 ? GrB_FP64 : GrB_BOOL;
         GB_Obj *o = gb_new_object(GB_KIND_MATRIX, t, nr, n);
         try {
@@ -98,7 +112,7 @@ extern "C" GrB_Info GxB_Matrix_rmat(GrB_Matrix *A, int scale, int edge_factor, u
             const uint64_t s0 = rm_smix(seed);
             const uint64_t k1 = rm_smix(seed ^ 0x5851F42D4C957F2DULL) | 1ULL, k2 = rm_smix(seed ^ 0x14057B7EF767814FULL);
             hipLaunchKernelGGL(k_rmat_edges, dim3(8192), dim3(256), 0, gb_stream(), ne, scale, s0, k1, k2,
-                               (uint64_t)row_begin, (uint64_t)row_end, keys, cnt);
+                               (uint64_t)row_begin, (uint64_t)row_end, transpose, keys, cnt);
             GB_LAUNCH_CHECK();
             // sort all keys (dropped ones are ~0 and land at the end)
             {
@@ -136,7 +150,7 @@ extern "C" GrB_Info GxB_Matrix_rmat(GrB_Matrix *A, int scale, int edge_factor, u
                 vals = gb_malloc(nz * 8);
                 const uint64_t vs0 = rm_smix(value_seed ^ 0xA0761D6478BD642FULL);
                 hipLaunchKernelGGL(k_rmat_values, dim3(4096), dim3(256), 0, gb_stream(), rowptr, colidx, nr,
-                                   (int64_t)row_begin, vs0, values, vals);
+                                   (int64_t)row_begin, vs0, values, transpose, vals);
                 GB_LAUNCH_CHECK();
             }
             gb_install_csr(o, nr, n, nz, rowptr, colidx, vals, iso);

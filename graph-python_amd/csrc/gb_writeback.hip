@@ -61,6 +61,7 @@ void gb_make_vmask(gb_vmask &m, GB_Obj *M, const gb_desc &d, int64_t n) {
             m.bits = c;
         } else {
             m.bits = bv->bits;
+            m.count = M->d_nvals;  // kept current by every writer of M
         }
     } else {
         uint64_t *c = m.own.get<uint64_t>(gb_words(n));

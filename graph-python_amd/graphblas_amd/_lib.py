@@ -54,6 +54,7 @@ _SIGS = {
     "GxB_Matrix_device_view": [P, P], "GxB_Vector_device_view": [P, P],
     "GxB_Vector_device_touch": [P], "GxB_Matrix_prepare_transpose": [P],
     "GxB_Matrix_rmat": [P, E, E, U, E, U, I, I],
+    "GxB_Vector_bitmap_export": [P, P, I], "GxB_Vector_bitmap_import": [P, P, I],
 }
 for _t in TYPE_NAMES:
     _T = _CTYPES[_t]

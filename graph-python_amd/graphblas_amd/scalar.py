@@ -10,6 +10,20 @@ from .dtypes import FP64, lookup_dtype
 from .exceptions import EmptyObject, NoValue, check_status_carg
 
 
+class _CPtr:
+    """Pointer to a host C scalar output (recorded as &s_temp)."""
+
+    __slots__ = "array"
+    name = "&s_temp"
+
+    def __init__(self, array):
+        self.array = array
+
+    @property
+    def _carg(self):
+        return ctypes.c_void_p(self.array.ctypes.data)
+
+
 class Scalar(BaseType):
     _is_scalar = True
     ndim = 0
@@ -123,11 +137,21 @@ class ScalarExpression(BaseExpression):
     def construct_output(self, dtype=None, *, name=None):
         return Scalar(self.dtype if dtype is None else dtype, name=name)
 
-    def new(self, dtype=None, *, name=None, **opts):
+    def new(self, dtype=None, *, mask=None, name=None, **opts):
+        if mask is not None:
+            raise TypeError("Mask not allowed for Scalars")
         s = self.construct_output(dtype, name=name)
+        if not self._allow_empty and self.cfunc_name.endswith("reduce_Monoid_Scalar"):
+            # allow_empty=False: C-scalar reduce, an empty input yields the monoid identity
+            # (reference core/vector.py:1561 reduce -> GrB_Vector_reduce_<T>)
+            A = self.args[0]
+            kind = "Matrix" if A.ndim == 2 else "Vector"
+            dt = self.op.type
+            out = np.zeros(1, dt.np_type)
+            call(f"GrB_{kind}_reduce_{dt.name}", [_CPtr(out), None, self.op, A, None])
+            s.value = out[0].item()
+            return s
         s._update(self, opts=opts)
-        if not self._allow_empty and s.is_empty:
-            raise EmptyObject("reduction of an empty collection with allow_empty=False")
         return s
 
     @property

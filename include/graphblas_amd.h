@@ -290,9 +290,15 @@ GrB_Info GxB_Vector_device_view(GxB_DeviceView *view, const GrB_Vector v);
 /* Mark that the vector's bitmap/values were rewritten through a device view
  * (nvals recomputed on device, on the library stream). */
 GrB_Info GxB_Vector_device_touch(GrB_Vector v);
+/* Copy the first nwords 64-bit words of a vector's presence bitmap to /
+ * from device memory on the library stream (frontier exchange over RCCL).
+ * Import makes the vector iso-valued 1 (true) on every set bit. */
+GrB_Info GxB_Vector_bitmap_export(GrB_Vector v, void *dst_device, GrB_Index nwords);
+GrB_Info GxB_Vector_bitmap_import(GrB_Vector v, const void *src_device, GrB_Index nwords);
 /* Build a pattern R-MAT graph on the device (same generator as the oracle):
  * scale, edge factor, seed; values: 0 = BOOL iso true, 1 = INT64 [1,255],
- * 2 = FP64 [0,1).  Rows [row_begin, row_end) only (row shard), all columns. */
+ * 2 = FP64 [0,1); | 0x100 = generate A^T.  Rows [row_begin, row_end) only (row shard),
+ * all columns; row_end = 0 means all rows. */
 GrB_Info GxB_Matrix_rmat(GrB_Matrix *A, int scale, int edge_factor, uint64_t seed,
                          int values, uint64_t value_seed, GrB_Index row_begin,
                          GrB_Index row_end);

@@ -443,10 +443,19 @@ def test_rmat_device_matches_oracle(gb, scale):
 
 
 @pytest.mark.parametrize("scale", [10, 14, 16])
-def test_bfs_rmat_vs_oracle(gb, scale):
+@pytest.mark.parametrize("direction", [0, 1, 2])  # auto (device-chosen), pull only, push only
+def test_bfs_rmat_vs_oracle(gb, scale, direction):
     G = O.rmat(scale, 16, 42)
     r, c, _ = G.to_coo()
     A = gb.Matrix.from_coo(r, c, True, nrows=G.nrows, ncols=G.ncols)
+    gb.set_knob("spmv_direction", direction)
+    try:
+        _bfs_check(gb, G, A)
+    finally:
+        gb.set_knob("spmv_direction", 0)
+
+
+def _bfs_check(gb, G, A):
     for src in [int(np.argmax(np.diff(G.indptr))), 0, G.nrows // 3]:
         lev_ref, _, _ = O.bfs_levels(G, src)
         vv = gb.Vector(gb.INT32, G.nrows)
