@@ -373,3 +373,40 @@ GB_DEV T gb_shfl_xor(T v, int mask, int width) {
 }
 
 GB_DEV bool gb_bit(const uint64_t *bits, int64_t i) { return (bits[i >> 6] >> (i & 63)) & 1ULL; }
+
+// (bool) of one value of runtime type `code` (mask semantics: -0.0 is false, NaN true)
+GB_DEV bool gb_dyn_nonzero(const void *p, int code) {
+    switch (code) {
+        case GBAMD_T_BOOL:
+        case GBAMD_T_INT8:
+        case GBAMD_T_UINT8: return *(const uint8_t *)p != 0;
+        case GBAMD_T_INT16:
+        case GBAMD_T_UINT16: return *(const uint16_t *)p != 0;
+        case GBAMD_T_INT32:
+        case GBAMD_T_UINT32: return *(const uint32_t *)p != 0;
+        case GBAMD_T_INT64:
+        case GBAMD_T_UINT64: return *(const uint64_t *)p != 0;
+        case GBAMD_T_FP32: return *(const float *)p != 0.0f;
+        case GBAMD_T_FP64: return *(const double *)p != 0.0;
+        default: return true;
+    }
+}
+
+// Add v (per thread) into *global with ONE atomic per block: wave shuffle
+// reduction, then the block's waves through LDS.  Every thread of the block
+// must call it (it contains a barrier).  Same-address atomics from every wave
+// of a large grid serialise at the memory side (tens of microseconds per
+// 10^4 adds), so counters are always reduced per block first.
+GB_DEV void gb_block_add(unsigned long long v, unsigned long long *global) {
+    __shared__ unsigned long long part[16];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    const int wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    if ((threadIdx.x & 63) == 0) part[wid] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long s = 0;
+        for (int w = 0; w < nw; w++) s += part[w];
+        if (s) atomicAdd(global, s);
+    }
+    __syncthreads();
+}

@@ -233,9 +233,13 @@ struct gb_vmask {
     const uint64_t *bits = nullptr;  // nullptr: no mask
     bool comp = false;
     const int64_t *count = nullptr;  // device count of set mask bits, when known
+    // value mask of an iso vector, left unmaterialised (only when the caller allows it):
+    // the mask is `bits` if the device value *iso_val is nonzero, else empty
+    const void *iso_val = nullptr;
+    int iso_code = -1;
     gb_scratch own;
 };
-void gb_make_vmask(gb_vmask &m, GB_Obj *M, const gb_desc &d, int64_t n);
+void gb_make_vmask(gb_vmask &m, GB_Obj *M, const gb_desc &d, int64_t n, bool allow_iso_value = false);
 
 struct gb_mmask {
     bool present = false, comp = false;

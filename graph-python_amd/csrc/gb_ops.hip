@@ -118,7 +118,7 @@ __global__ void k_ewise_vec(int64_t n, int op, bool add, const uint64_t *__restr
             mine += __popcll(w);
         }
     }
-    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(cnt, mine);
+    gb_block_add(mine, cnt);
 }
 
 template <class X, class Z, bool FILL>
@@ -194,7 +194,7 @@ static void do_ewise(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, GrB_BinaryOp op, 
             using X = decltype(x);
             using Z = decltype(z);
             if (n)
-                hipLaunchKernelGGL((k_ewise_vec<X, Z>), dim3(ops_grid(n)), dim3(OPS_BLOCK), 0, gb_stream(), n,
+                hipLaunchKernelGGL((k_ewise_vec<X, Z>), dim3(ops_grid(n, 1024)), dim3(OPS_BLOCK), 0, gb_stream(), n,
                                    op->opcode, add, ua.bits, (const X *)xa, ua.iso, ub.bits, (const X *)xb, ub.iso,
                                    T.bits, (Z *)T.dense, (unsigned long long *)T.d_nvals);
         });
@@ -416,18 +416,17 @@ static GrB_BinaryOp second_of(int code) {
 template <class T>
 __global__ __launch_bounds__(OPS_BLOCK) void k_assign_all_scalar(
     int64_t n, uint64_t *__restrict__ cbits, T *__restrict__ cvals, const uint64_t *__restrict__ mbits, bool mcomp,
-    bool replace, T x, unsigned long long *__restrict__ count) {
-    unsigned long long mine = 0;
+    const void *miso, int miso_code, bool replace, T x, unsigned long long *__restrict__ count) {
+    // value mask over an iso vector: the mask is its structure if the value is true, else empty
+    const bool iso_true = miso ? gb_dyn_nonzero(miso, miso_code) : true;
+    long long delta = 0;  // change of nvals(C); added to the count C already holds
     for (int64_t base = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) & ~63LL; base < n;
          base += (int64_t)gridDim.x * blockDim.x) {
         const int lane = threadIdx.x & 63;
         const int64_t w = base >> 6;
         const int64_t i = base + lane;
-        uint64_t mword = mbits ? mbits[w] : 0;
-        if (mbits && !mcomp && mword == 0 && !replace) {
-            if (lane == 0) mine += __popcll(cbits[w]);
-            continue;
-        }
+        uint64_t mword = (mbits && iso_true) ? mbits[w] : 0;
+        if (mbits && !mcomp && mword == 0 && !replace) continue;
         const uint64_t cword = cbits[w];
         bool inr = i < n;
         bool m = inr && (mbits ? ((((mword >> lane) & 1ULL) != 0) != mcomp) : !mcomp);
@@ -436,12 +435,39 @@ __global__ __launch_bounds__(OPS_BLOCK) void k_assign_all_scalar(
         bool have = m || (!replace && c && inr);
         unsigned long long word = __ballot(have);
         if (lane == 0) {
-            cbits[w] = word;
-            mine += __popcll(word);
+            if (word != cword) cbits[w] = word;
+            delta += (long long)__popcll(word) - (long long)__popcll(cword);
         }
     }
-    for (int off = 32; off > 0; off >>= 1) mine += __shfl_xor(mine, off, 64);
-    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(count, mine);
+    gb_block_add((unsigned long long)delta, count);
+}
+
+// w<M>(:) = x, M a plain (non-complemented) mask, no replace: a thread per
+// 64-bit word; only words with selected bits are touched.
+template <class T>
+__global__ __launch_bounds__(OPS_BLOCK) void k_assign_mask_words(int64_t nwords, uint64_t *__restrict__ cbits,
+                                                                 T *__restrict__ cvals,
+                                                                 const uint64_t *__restrict__ mbits, const void *miso,
+                                                                 int miso_code, T x,
+                                                                 unsigned long long *__restrict__ count) {
+    const bool iso_true = miso ? gb_dyn_nonzero(miso, miso_code) : true;
+    long long delta = 0;
+    if (iso_true) {
+        for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nwords;
+             w += (int64_t)gridDim.x * blockDim.x) {
+            uint64_t m = mbits[w];
+            if (!m) continue;
+            const uint64_t c = cbits[w], nwd = c | m;
+            if (nwd != c) cbits[w] = nwd;
+            delta += (long long)__popcll(nwd) - (long long)__popcll(c);
+            while (m) {
+                const int b = __ffsll((unsigned long long)m) - 1;
+                m &= m - 1;
+                cvals[(w << 6) + b] = x;
+            }
+        }
+    }
+    gb_block_add((unsigned long long)delta, count);
 }
 
 static bool assign_all_scalar_fast(GB_Obj *w, GB_Obj *mask, const char *xc, const gb_desc &d) {
@@ -449,7 +475,7 @@ static bool assign_all_scalar_fast(GB_Obj *w, GB_Obj *mask, const char *xc, cons
     const int64_t n = w->nrows;
     const size_t ts = w->type->size;
     gb_vmask m;
-    gb_make_vmask(m, mask, d, n);
+    gb_make_vmask(m, mask, d, n, true);
     if (!m.bits && !m.comp) {
         // no mask: w becomes full and iso x
         int64_t nw = gb_words(n);
@@ -477,15 +503,24 @@ static bool assign_all_scalar_fast(GB_Obj *w, GB_Obj *mask, const char *xc, cons
         w->dense = full;
         w->iso = false;
     }
-    gb_memset(w->d_nvals, 0, sizeof(int64_t));
-    unsigned grid = (unsigned)std::min<int64_t>((n + OPS_BLOCK - 1) / OPS_BLOCK, 8192);
+    if (!w->d_nvals) {
+        w->d_nvals = gb_malloc_n<int64_t>(1);
+        gb_memset(w->d_nvals, 0, sizeof(int64_t));
+    }
+    unsigned grid = (unsigned)std::min<int64_t>((n + OPS_BLOCK - 1) / OPS_BLOCK, 1024);
     gb_with_type(w->type->code, [&](auto z) {
         using T = decltype(z);
         T xv;
         memcpy(&xv, xc, sizeof(T));
-        if (n)
+        if (n && m.bits && !m.comp && !d.replace)
+            hipLaunchKernelGGL(k_assign_mask_words<T>,
+                               dim3((unsigned)std::min<int64_t>((gb_words(n) + OPS_BLOCK - 1) / OPS_BLOCK, 1024)),
+                               dim3(OPS_BLOCK), 0, gb_stream(), gb_words(n), w->bits, (T *)w->dense, m.bits, m.iso_val,
+                               m.iso_code, xv, (unsigned long long *)w->d_nvals);
+        else if (n)
             hipLaunchKernelGGL(k_assign_all_scalar<T>, dim3(grid), dim3(OPS_BLOCK), 0, gb_stream(), n, w->bits,
-                               (T *)w->dense, m.bits, m.comp, d.replace, xv, (unsigned long long *)w->d_nvals);
+                               (T *)w->dense, m.bits, m.comp, m.iso_val, m.iso_code, d.replace, xv,
+                               (unsigned long long *)w->d_nvals);
     });
     GB_LAUNCH_CHECK();
     w->nvals_valid = false;

@@ -38,7 +38,7 @@ __global__ void k_vmask_values(const uint64_t *__restrict__ bits, const T *__res
     }
 }
 
-void gb_make_vmask(gb_vmask &m, GB_Obj *M, const gb_desc &d, int64_t n) {
+void gb_make_vmask(gb_vmask &m, GB_Obj *M, const gb_desc &d, int64_t n, bool allow_iso_value) {
     m.comp = d.comp;
     if (!M) {
         if (d.comp) {  // ~NULL: nothing is selected
@@ -63,6 +63,10 @@ void gb_make_vmask(gb_vmask &m, GB_Obj *M, const gb_desc &d, int64_t n) {
             m.bits = bv->bits;
             m.count = M->d_nvals;  // kept current by every writer of M
         }
+    } else if (allow_iso_value && bv->iso && !bv->own.n) {
+        m.bits = bv->bits;
+        m.iso_val = bv->vals;
+        m.iso_code = bv->tcode;
     } else {
         uint64_t *c = m.own.get<uint64_t>(gb_words(n));
         gb_with_type(bv->tcode, [&](auto z) {
@@ -184,7 +188,7 @@ __global__ __launch_bounds__(WB_BLOCK) void k_vec_merge(
             mine += __popcll(word);
         }
     }
-    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(count, mine);
+    gb_block_add(mine, count);
 }
 
 static void cast_vec_result(gb_vec_result &T, int code) {
@@ -245,7 +249,7 @@ void gb_writeback_vector(GB_Obj *C, gb_vec_result &T, GB_Obj *M, const gb_desc &
     if (n) {
         gb_with_type(wcode, [&](auto z) {
             using W = decltype(z);
-            hipLaunchKernelGGL(k_vec_merge<W>, dim3(wb_grid(n)), dim3(WB_BLOCK), 0, gb_stream(), n, cv.bits,
+            hipLaunchKernelGGL(k_vec_merge<W>, dim3(wb_grid(n, 1024)), dim3(WB_BLOCK), 0, gb_stream(), n, cv.bits,
                                (const W *)cvals, c_iso, T.bits, (const W *)T.dense, T.iso, mask.bits, mask.comp,
                                d.replace, accum ? accum->opcode : -1, obits, (W *)ovals,
                                (unsigned long long *)cnt);
