@@ -11,9 +11,12 @@ device (GxB_Matrix_rmat) and its CSC cache is built before timing (ingest).
 
 value  = GTEPS = edges of the reached component, summed over the K timed BFS,
          / wall time of the K BFS (max over ranks).
-roofline: dominant kernel = the masked pull SpMV (k_spmv_pull inside GrB_vxm),
-timed with HIP events on the library's stream; algorithmic bytes per BFS =
-SURVEY §8(d): 4*nnz + 8*(n+1) + L*3*ceil(n/8).
+value is total edges / wall time; gteps_harmonic_mean is Graph500's per-root
+harmonic mean.  roofline: the dominant op is the masked SpMV (GrB_vxm: the
+k_dir_prep + k_iso_work launches), timed with HIP events on the library's
+stream in a separate pass after the timed region (one BFS per root);
+algorithmic bytes per BFS = SURVEY §8(d) config 3: 4*nnz + 8*(n+1) +
+L*3*ceil(n/8), divided evenly over the BFS's L launches.
 cpu_baseline: the oracle's GraphBLAS-loop BFS (oracle/gb_oracle.c
 or_bfs_graphblas) on a bounded sample of the same roots, one host thread.
 
@@ -228,11 +231,13 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    ev_pairs.clear()
     level_counts.clear()
+    per_bfs = []
     t0 = time.perf_counter()
     for s in range(args.steps):
-        bfs(roots[s % len(roots)], True)
+        tb = time.perf_counter()
+        bfs(roots[s % len(roots)], False)  # ends on the host-side nvals read: the BFS is complete
+        per_bfs.append(time.perf_counter() - tb)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -242,14 +247,24 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev_pairs)
-    launches = len(ev_pairs)
 
     total_edges = sum(edges[s % len(roots)] for s in range(args.steps))
     gteps = total_edges / elapsed / 1e9
+    # Graph500 convention: harmonic mean of the per-root TEPS (rank 0's clock)
+    hm = len(per_bfs) / sum(t / edges[s % len(roots)] for s, t in enumerate(per_bfs)) / 1e9
+
+    # roofline pass (after the timed region): HIP events on the library stream around
+    # every GrB_vxm / GrB_mxv (k_dir_prep + k_iso_work), one BFS per root
+    ev_pairs.clear()
+    level_counts.clear()
+    for src in roots:
+        bfs(src, True)
+    torch.cuda.synchronize()
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev_pairs)
+    launches = len(ev_pairs)
     levels_total = sum(level_counts)
-    # per-rank algorithmic bytes of the SpMV kernels (each rank streams its own shard)
-    alg_bytes = args.steps * (4 * int(ap[-1]) + 8 * (nloc + 1)) + levels_total * 3 * ((n + 7) // 8)
+    # per-rank algorithmic bytes of the SpMV calls (each rank streams its shard)
+    alg_bytes = len(roots) * (4 * int(ap[-1]) + 8 * (nloc + 1)) + levels_total * 3 * ((n + 7) // 8)
     achieved = alg_bytes / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else None
     traffic = None
     if os.path.exists(args.traffic_file):
@@ -257,6 +272,19 @@ def main():
             traffic = json.load(open(args.traffic_file)).get("bytes_per_launch")
         except Exception:
             traffic = None
+    # measured stream-copy ceiling (device-to-device copy of 2 GiB: read + write bytes)
+    copy_gbs = None
+    if rank == 0:
+        xs = torch.empty(1 << 31, dtype=torch.uint8, device="cuda")
+        ys = torch.empty_like(xs)
+        ys.copy_(xs)
+        torch.cuda.synchronize()
+        c0 = time.perf_counter()
+        for _ in range(5):
+            ys.copy_(xs)
+        torch.cuda.synchronize()
+        copy_gbs = 5 * 2 * xs.numel() / (time.perf_counter() - c0) / 1e9
+        del xs, ys
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -298,8 +326,10 @@ def main():
                        "parallelism": f"1-D row shards x{world}" if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": (achieved / PEAK_HBM_GBS) if achieved else None, "traffic": traffic,
-                         "kernel": "k_spmv_pull", "kernel_ms_total": kern_ms, "launches": launches,
-                         "alg_bytes_rank0": alg_bytes},
+                         "kernel": "GrB_vxm = k_dir_prep + k_iso_work", "avg_launch_us": kern_ms * 1e3 / launches,
+                         "launches": launches, "alg_bytes_per_launch": alg_bytes / launches,
+                         "stream_copy_GBs": copy_gbs},
+            "gteps_harmonic_mean": hm,
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,
             "ingest_s": ingest_s,

@@ -64,6 +64,19 @@ hipStream_t gb_stream() {
 
 void gb_sync() { GB_HIP(hipStreamSynchronize(gb_stream())); }
 
+unsigned long long *gb_device_state() {
+    static std::mutex mu;
+    static unsigned long long *st = nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!st) {
+        gb_require_init();
+        GB_HIP(hipMalloc(&st, GB_STATE_WORDS * sizeof(unsigned long long)));
+        GB_HIP(hipMemset(st, 0, GB_STATE_WORDS * sizeof(unsigned long long)));
+        GB_HIP(hipDeviceSynchronize());
+    }
+    return st;
+}
+
 int64_t gb_knob(const char *key) {
     std::lock_guard<std::mutex> lk(g_knob_mu);
     auto it = g_knobs.find(key);

@@ -11,6 +11,7 @@
 #include <type_traits>
 
 #include "../../include/gbamd_codes.h"
+#include "gb_state.h"
 
 #define GB_DEV __device__ __forceinline__
 #define GB_HD __host__ __device__ __forceinline__
@@ -397,6 +398,53 @@ GB_DEV bool gb_dyn_nonzero(const void *p, int code) {
 // must call it (it contains a barrier).  Same-address atomics from every wave
 // of a large grid serialise at the memory side (tens of microseconds per
 // 10^4 adds), so counters are always reduced per block first.
+// Sum over the block, result in thread 0.  All threads must call.
+GB_DEV long long gb_block_sum(long long v) {
+    __shared__ long long part[16];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    const int wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    if ((threadIdx.x & 63) == 0) part[wid] = v;
+    __syncthreads();
+    long long s = 0;
+    if (threadIdx.x == 0)
+        for (int w = 0; w < nw; w++) s += part[w];
+    __syncthreads();
+    return s;
+}
+
+// Grid-wide sum without a same-address pile-up.  Adds to one device-scope
+// counter serialise at the memory side (about 12 ns each), so each block adds
+// (sum << 20 | 1) to one of GB_GRID_SHARDS counters 256 B apart; the last
+// arrival of a shard forwards the shard's sum to a root counter, and the last
+// arrival there receives the grand total.  Every block of the grid must call it
+// exactly once; it leaves the counters zeroed.  Returns true in thread 0 of
+// exactly one block, with *total set.  Needs |sum| < 2^43, grid < 2^25 blocks.
+GB_DEV bool gb_grid_sum(long long v, unsigned long long *st, long long *total) {
+    v = gb_block_sum(v);
+    if (threadIdx.x != 0) return false;
+    const unsigned nb = gridDim.x;
+    const unsigned s = blockIdx.x % GB_GRID_SHARDS;
+    const unsigned in_shard = (nb - s + GB_GRID_SHARDS - 1) / GB_GRID_SHARDS;
+    unsigned long long *cs = st + (size_t)s * GB_GRID_STRIDE;
+    const long long old = (long long)atomicAdd(cs, ((unsigned long long)v << 20) + 1ULL);
+    if ((unsigned)(old & 0xFFFFF) + 1 != in_shard) return false;
+    atomicExch(cs, 0ULL);
+    const long long shard_sum = (old >> 20) + v;
+    const unsigned nshards = nb < GB_GRID_SHARDS ? nb : GB_GRID_SHARDS;
+    unsigned long long *root = st + (size_t)GB_GRID_SHARDS * GB_GRID_STRIDE;
+    const long long o2 = (long long)atomicAdd(root, ((unsigned long long)shard_sum << 20) + 1ULL);
+    if ((unsigned)(o2 & 0xFFFFF) + 1 != nshards) return false;
+    atomicExch(root, 0ULL);
+    *total = (o2 >> 20) + shard_sum;
+    return true;
+}
+
+// *global += grid-wide sum of v (one add on *global).  All threads of every block must call.
+GB_DEV void gb_grid_add(long long v, unsigned long long *global, unsigned long long *st) {
+    long long t;
+    if (gb_grid_sum(v, st, &t) && t) atomicAdd(global, (unsigned long long)t);
+}
+
 GB_DEV void gb_block_add(unsigned long long v, unsigned long long *global) {
     __shared__ unsigned long long part[16];
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);

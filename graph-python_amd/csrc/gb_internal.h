@@ -14,6 +14,7 @@
 #include <string>
 
 #include "../../include/gbamd_codes.h"
+#include "gb_state.h"
 #include "../../include/graphblas_amd.h"
 
 #define GB_MAGIC 0x6d614d424731ULL   // live object
@@ -77,6 +78,10 @@ struct GB_Matrix_opaque {
     int64_t *t_rowptr;
     int32_t *t_colidx;
     void *t_vals;
+    // cached hub-chunk tables of the CSR (0) and CSC (1) orientation, built by
+    // gb_view_hubs (gb_mxv.hip); dropped with the transpose
+    int32_t *hub_tab[2];
+    int64_t hub_n[2], hub_H[2];
     // ---- bitmap (kind == VECTOR / SCALAR); length n = nrows (ncols == 1)
     uint64_t *bits;      // [ceil(n/64)]
     void *dense;         // [n] or [1] when iso
@@ -126,7 +131,9 @@ GrB_Info gb_api(GB_Obj *errobj, F &&body) {
 hipStream_t gb_stream();
 void gb_require_init();
 void gb_sync();
-int64_t gb_knob(const char *key);  // tuning knobs (0 = auto)
+int64_t gb_knob(const char *key);
+// persistent zeroed device words (layout: gb_state.h), allocated on first use
+unsigned long long *gb_device_state();  // tuning knobs (0 = auto)
 
 // device memory (stream-ordered pool on the library stream)
 void *gb_malloc(size_t bytes);        // throws GrB_OUT_OF_MEMORY
@@ -175,9 +182,14 @@ struct gb_csr_view {
     const void *vals = nullptr;
     bool iso = false;
     int tcode = 0;
+    // hub chunks (rows longer than hub_H cut into hub_H-edge pieces): pairs (row, piece)
+    const int32_t *hubs = nullptr;
+    int64_t nhubs = 0, hub_H = 0;
     gb_scratch own;
 };
 void gb_get_csr(gb_csr_view &v, GB_Obj *A);
+// attach the cached hub-chunk table of matrix A's orientation (0 CSR, 1 CSC) to v
+void gb_view_hubs(gb_csr_view &v, GB_Obj *A, int orient, int64_t H);
 // CSC of A (i.e. CSR of A^T), cached on the object when A is a matrix.
 void gb_get_csc(gb_csr_view &v, GB_Obj *A);
 // Values of a CSR view cast to type `code` (returns the view's own pointer if same type).

@@ -14,15 +14,17 @@
 // whole 64-bit words; one counter atomic per block.
 //
 // Iso results (BFS lor_land / any_pair: only presence is computed) take the
-// direction-optimised path, three launches per call:
-//   k_dir_prep  frontier edge count m_f (block partials; the last block applies
-//               Beamer's rule m_f * alpha < m_u on the device), hub chunks,
-//               zeroed output, iso value;
-//   k_push      top-down: each frontier row of the other orientation of A'
-//               sets the bits of its unmasked targets with atomicOr; rows with
-//               more than H edges are split into H-edge chunks over many waves;
-//   k_pull_iso  bottom-up: one lane per output row, stop at the first k in u.
-// The direction not chosen returns at once; no host round trip.
+// direction-optimised path, two launches per call:
+//   k_dir_prep  frontier edge count m_f (grid-wide sum; the block completing it
+//               applies Beamer's rule m_f * alpha < m_u on the device), zeroed
+//               output, iso value;
+//   k_iso_work  the chosen direction --
+//     push (top-down): each frontier row of the other orientation of A' sets
+//       the bits of its unmasked targets with atomicOr; a wave spreads the
+//       rows of one frontier word over its lanes; rows longer than H are cut
+//       into H-edge chunks (a table cached on the matrix) spread over waves;
+//     pull (bottom-up): one lane per output row, stop at the first k in u.
+// No host round trip is needed for the choice.
 #include <mutex>
 
 #include "gb_dispatch.cuh"
@@ -30,14 +32,14 @@
 
 #define SPMV_BLOCK 256
 #define SPMV_TILE 256
-#define PREP_BLOCKS 256
 
 template <class SR, class X, class Z, bool FLIP>
 __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_pull(
     SR sr, int64_t nrows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ colidx,
     const X *__restrict__ avals, bool a_iso, const uint64_t *__restrict__ ubits,
     const X *__restrict__ uvals, bool u_iso, const uint64_t *__restrict__ mbits, bool mcomp, int lg,
-    uint64_t *__restrict__ tbits, Z *__restrict__ tvals, unsigned long long *__restrict__ tcount) {
+    uint64_t *__restrict__ tbits, Z *__restrict__ tvals, unsigned long long *__restrict__ tcount,
+    unsigned long long *__restrict__ gst) {
     __shared__ unsigned long long words[SPMV_TILE / 64];
     const int G = 1 << lg;
     const int gid = threadIdx.x >> lg;
@@ -106,16 +108,15 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_pull(
             }
         }
     }
-    gb_block_add(threadIdx.x < SPMV_TILE / 64 ? mycount : 0, tcount);
+    gb_grid_add(threadIdx.x < SPMV_TILE / 64 ? (long long)mycount : 0, tcount, gst);
 }
 
 // ---------------------------------------------------------------- iso results (BFS)
-// Persistent per-process state of the direction-optimised path (zeroed once;
-// every gb_spmv leaves it as it found it):
-//   [0] prep-block ticket (the last prep block resets it)
-//   [1] chosen direction: 1 push, 0 pull (written by the last prep block)
-//   [2] number of hub chunks listed by prep (reset by the pull kernel)
-enum { ST_TICKET = 0, ST_PUSH = 1, ST_NCHUNKS = 2, ST_WORDS = 8 };
+// Direction state words (gb_state.h, GB_DIR_STATE_OFFSET; zero between calls
+// except ST_PUSH, which every prep rewrites):
+//   [ST_PUSH]     chosen direction: 1 push, 0 pull (written by the last prep block)
+enum { ST_PUSH = 0 };
+#define PULL_U 4  // bitmap words per wave step (independent loads in flight)
 
 struct gb_dir_rule {
     const int64_t *mask_count;  // device count of set mask bits (nullptr: unknown)
@@ -124,38 +125,38 @@ struct gb_dir_rule {
     int force_push;
 };
 
-// Prep: per-block (m_f, n_f) of the frontier in the push orientation; hub rows
-// (more than H edges) are cut into H-edge chunks listed in `chunks`; zeroes the
-// output bitmap and count; writes the iso result value.  The last block to
-// finish sums the partials and applies Beamer's rule m_f * alpha < m_u.
+// Prep: m_f = edges of the frontier in the push orientation (one lane per
+// frontier bit); zeroes the output bitmap and count; writes the iso result
+// value.  The block that completes the grid-wide sum of m_f applies
+// Beamer's rule m_f * alpha < m_u and stores the direction.
 template <class SR, class X, class Z, bool FLIP>
 __global__ __launch_bounds__(SPMV_BLOCK) void k_dir_prep(
-    SR sr, const uint64_t *__restrict__ ubits, int64_t nwords_u, const int64_t *__restrict__ prow, int64_t H,
-    int64_t *__restrict__ chunks, unsigned long long *__restrict__ part, unsigned long long *__restrict__ state,
+    SR sr, const uint64_t *__restrict__ ubits, int64_t nwords_u, const int64_t *__restrict__ prow,
+    unsigned long long *__restrict__ gst, unsigned long long *__restrict__ dst,
     uint64_t *__restrict__ tbits, int64_t nwords_out, unsigned long long *__restrict__ tcount, const X *avals,
     const X *uvals, Z *iso_out, gb_dir_rule rule) {
-    unsigned long long mf = 0;
-    const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t w = tid; w < nwords_u; w += nthr) {
-        uint64_t word = ubits[w];
-        while (word) {
-            const int b = __ffsll((unsigned long long)word) - 1;
-            word &= word - 1;
-            const int64_t k = (w << 6) + b;
-            const int64_t deg = prow[k + 1] - prow[k];
-            mf += deg;
-            if (deg > H) {
-                const int64_t c = (deg + H - 1) / H;
-                const int64_t base = (int64_t)atomicAdd(&state[ST_NCHUNKS], (unsigned long long)c);
-                for (int64_t i = 0; i < c; i++) {
-                    chunks[2 * (base + i)] = k;
-                    chunks[2 * (base + i) + 1] = i;
-                }
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    long long mf = 0;
+    for (int64_t w0 = wave * PULL_U; w0 < nwords_u; w0 += nwaves * PULL_U) {
+        const int64_t wl = w0 + (lane & (PULL_U - 1));
+        const uint64_t mine = wl < nwords_u ? ubits[wl] : 0;
+        int64_t deg[PULL_U];
+#pragma unroll
+        for (int u = 0; u < PULL_U; u++) {
+            const uint64_t word = __shfl(mine, u, 64);
+            deg[u] = 0;
+            if ((word >> lane) & 1ULL) {
+                const int64_t k = ((w0 + u) << 6) + lane;
+                deg[u] = prow[k + 1] - prow[k];
             }
         }
+#pragma unroll
+        for (int u = 0; u < PULL_U; u++) mf += deg[u];
     }
-    for (int64_t w = tid; w < nwords_out; w += nthr) tbits[w] = 0;
+    const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    for (int64_t w = tid; w < nwords_out; w += (int64_t)gridDim.x * blockDim.x) tbits[w] = 0;
     if (tid == 0) {
         *tcount = 0;
         if (iso_out) {
@@ -163,31 +164,8 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_dir_prep(
             *iso_out = FLIP ? sr.mult(b, a, 0, 0, 0) : sr.mult(a, b, 0, 0, 0);
         }
     }
-    __shared__ unsigned long long red[SPMV_BLOCK / 64];
-    __shared__ int s_last;
-    for (int off = 32; off > 0; off >>= 1) mf += __shfl_xor(mf, off, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mf;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long a = 0;
-        for (int i = 0; i < SPMV_BLOCK / 64; i++) a += red[i];
-        part[blockIdx.x] = a;
-        __threadfence();
-        s_last = atomicAdd(&state[ST_TICKET], 1ULL) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    // last block: every partial is visible (each was fenced before its ticket)
-    __threadfence();
-    unsigned long long v = 0;
-    for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x) v += ((volatile unsigned long long *)part)[i];
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long total = 0;
-        for (int i = 0; i < SPMV_BLOCK / 64; i++) total += red[i];
+    long long total;
+    if (gb_grid_sum(mf, gst, &total)) {
         int64_t open = rule.n_out;  // rows the pull kernel would visit
         if (rule.mask_count) {
             const int64_t mc = *rule.mask_count;
@@ -195,147 +173,269 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_dir_prep(
         }
         const double avg = rule.n_out ? (double)rule.nnz / (double)rule.n_out : 0.0;
         const bool push = rule.force_push || ((double)total * (double)rule.alpha < (double)open * avg);
-        state[ST_PUSH] = push ? 1ULL : 0ULL;
-        state[ST_TICKET] = 0;
+        dst[ST_PUSH] = push ? 1ULL : 0ULL;
     }
 }
 
-// set output bits for edges [p0, p1) of one row; 4 loads in flight per lane
-__device__ __forceinline__ unsigned long long gb_push_range(int64_t p0, int64_t p1, int lane,
-                                                            const int32_t *__restrict__ pcol,
-                                                            const uint64_t *__restrict__ mbits, bool mcomp,
-                                                            unsigned long long *__restrict__ tbits) {
-    unsigned long long added = 0;
-    for (int64_t p = p0 + lane; p < p1; p += 256) {
-        int32_t j[4];
-        bool ok[4];
+// set the output bits of up to 4 targets per lane (unmasked, not yet set);
+// returns how many bits this lane turned on
+__device__ __forceinline__ long long gb_push_targets(const int32_t (&j)[4], bool (&ok)[4],
+                                                     const uint64_t *__restrict__ mbits, bool mcomp,
+                                                     unsigned long long *__restrict__ tbits) {
+    if (mbits) {
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int64_t q = p + 64 * u;
-            ok[u] = q < p1;
-            j[u] = ok[u] ? pcol[q] : 0;
-        }
-        if (mbits) {
+        for (int u = 0; u < 4; u++)
+            if (ok[u]) ok[u] = gb_bit(mbits, j[u]) != mcomp;
+    }
+    unsigned long long cur[4];
 #pragma unroll
-            for (int u = 0; u < 4; u++)
-                if (ok[u]) ok[u] = gb_bit(mbits, j[u]) != mcomp;
-        }
-        unsigned long long cur[4];
+    for (int u = 0; u < 4; u++) cur[u] = ok[u] ? tbits[j[u] >> 6] : ~0ULL;
+    long long added = 0;
 #pragma unroll
-        for (int u = 0; u < 4; u++) cur[u] = ok[u] ? tbits[j[u] >> 6] : ~0ULL;
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const unsigned long long m = 1ULL << (j[u] & 63);
-            if (ok[u] && !(cur[u] & m)) {
-                unsigned long long old = atomicOr(&tbits[j[u] >> 6], m);
-                if (!(old & m)) added++;
-            }
+    for (int u = 0; u < 4; u++) {
+        const unsigned long long m = 1ULL << (j[u] & 63);
+        if (ok[u] && !(cur[u] & m)) {
+            const unsigned long long old = atomicOr(&tbits[j[u] >> 6], m);
+            if (!(old & m)) added++;
         }
     }
     return added;
 }
 
-// Push (top-down): units [0, nchunks) are hub chunks, then one unit per
-// frontier word (its rows of at most H edges).  One wave per unit.
-__global__ __launch_bounds__(SPMV_BLOCK) void k_push(
-    int64_t nwords_u, const uint64_t *__restrict__ ubits, const int64_t *__restrict__ prow,
-    const int32_t *__restrict__ pcol, const uint64_t *__restrict__ mbits, bool mcomp,
-    unsigned long long *__restrict__ tbits, unsigned long long *__restrict__ tcount,
-    const int64_t *__restrict__ chunks, const unsigned long long *__restrict__ state, int64_t H) {
-    if (!state[ST_PUSH]) return;
+// Push (top-down).  Units [0, nhubs) are the matrix's hub chunks (rows longer
+// than H cut into H-edge pieces, a static table): a wave takes a chunk if its
+// row is in the frontier, 256 edges a step.  Then one unit per frontier word:
+// the rows of its frontier vertices (at most H edges each) are concatenated
+// and spread over the wave's lanes, 256 edges a step (wave prefix sum of the
+// row lengths; a lane finds the row of its edge by binary search over it).
+__device__ __forceinline__ long long gb_push_phase(int64_t nwords_u, const uint64_t *__restrict__ ubits,
+                                                  const int64_t *__restrict__ prow, const int32_t *__restrict__ pcol,
+                                                  const int32_t *__restrict__ hubs, int64_t nhubs, int64_t H,
+                                                  const uint64_t *__restrict__ mbits, bool mcomp,
+                                                  unsigned long long *__restrict__ tbits) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    const int64_t nch = (int64_t)state[ST_NCHUNKS];
-    unsigned long long added = 0;
-    for (int64_t unit = wave; unit < nch + nwords_u; unit += nwaves) {
-        if (unit < nch) {
-            const int64_t k = chunks[2 * unit], c = chunks[2 * unit + 1];
+    long long added = 0;
+    for (int64_t unit = wave; unit < nhubs + nwords_u; unit += nwaves) {
+        if (unit < nhubs) {
+            const int64_t k = hubs[2 * unit], c = hubs[2 * unit + 1];
+            if (!gb_bit(ubits, k)) continue;
             const int64_t p0 = prow[k] + c * H, pe = prow[k + 1];
-            added += gb_push_range(p0, (p0 + H < pe) ? p0 + H : pe, lane, pcol, mbits, mcomp, tbits);
+            const int64_t p1 = (p0 + H < pe) ? p0 + H : pe;
+            for (int64_t p = p0 + lane; p < p1; p += 256) {
+                int32_t j[4];
+                bool ok[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    ok[u] = p + 64 * u < p1;
+                    j[u] = ok[u] ? pcol[p + 64 * u] : 0;
+                }
+                added += gb_push_targets(j, ok, mbits, mcomp, tbits);
+            }
             continue;
         }
-        const int64_t w = unit - nch;
-        uint64_t word = ubits[w];
-        while (word) {
-            const int b = __ffsll((unsigned long long)word) - 1;
-            word &= word - 1;
-            const int64_t k = (w << 6) + b;
-            const int64_t p0 = prow[k], p1 = prow[k + 1];
-            if (p1 - p0 > H) continue;  // a hub: done by its chunks
-            added += gb_push_range(p0, p1, lane, pcol, mbits, mcomp, tbits);
+        const int64_t w = unit - nhubs;
+        const uint64_t word = ubits[w];
+        if (!word) continue;
+        int64_t p0 = 0;
+        int len = 0;
+        if ((word >> lane) & 1ULL) {
+            const int64_t k = (w << 6) + lane;
+            p0 = prow[k];
+            const int64_t d = prow[k + 1] - p0;
+            len = d > H ? 0 : (int)d;  // hubs: done by their chunks
+        }
+        int incl = len;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += y;
+        }
+        const int excl = incl - len;
+        const int total = __shfl(incl, 63, 64);
+        for (int e0 = 0; e0 < total; e0 += 256) {
+            int32_t j[4];
+            bool ok[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int e = e0 + lane + 64 * u;
+                int lo = 0;  // owner row: first lane whose inclusive prefix exceeds e
+#pragma unroll
+                for (int st = 32; st > 0; st >>= 1)
+                    if (__shfl(incl, lo + st - 1, 64) <= e) lo += st;
+                const int64_t ps = __shfl(p0, lo, 64);
+                const int ex = __shfl(excl, lo, 64);
+                ok[u] = e < total;
+                j[u] = ok[u] ? pcol[ps + (e - ex)] : 0;
+            }
+            added += gb_push_targets(j, ok, mbits, mcomp, tbits);
         }
     }
-    gb_block_add(added, tcount);
+    return added;
 }
 
-// Pull (bottom-up) for iso results: only presence is computed.  One wave per
-// 64-row bitmap word, one lane per row: a lane walks its own row two edges a
-// step (neighbouring rows are neighbouring in colidx, so the loads coalesce),
-// stopping at the first k present in u; rows still open after 8 edges are
-// finished by the whole wave, one row at a time, 256 edges a step.
-__global__ __launch_bounds__(SPMV_BLOCK) void k_pull_iso(
-    int64_t nrows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ colidx,
-    const uint64_t *__restrict__ ubits, const uint64_t *__restrict__ mbits, bool mcomp, uint64_t *__restrict__ tbits,
-    unsigned long long *__restrict__ tcount, unsigned long long *__restrict__ state) {
-    if (state) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) state[ST_NCHUNKS] = 0;  // k_push is done with it
-        if (state[ST_PUSH]) return;
-    }
+// Pull (bottom-up) for iso results: only presence is computed.  A wave takes
+// PULL_U 64-row bitmap words at a time, one lane per row of each: a lane walks
+// its own rows two edges a step (neighbouring rows are neighbouring in colidx,
+// so the loads coalesce), stopping at the first k present in u; rows still
+// open after 8 edges are finished eight at a time, eight lanes per row.
+__device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int64_t *__restrict__ rowptr,
+                                                      const int32_t *__restrict__ colidx,
+                                                      const uint64_t *__restrict__ ubits,
+                                                      const uint64_t *__restrict__ mbits, bool mcomp,
+                                                      uint64_t *__restrict__ tbits) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const int64_t nwords = (nrows + 63) >> 6;
-    unsigned long long cnt = 0;
-    for (int64_t w = wave; w < nwords; w += nwaves) {
-        uint64_t act = ~0ULL;
-        if (mbits) act = mcomp ? ~mbits[w] : mbits[w];
-        if (w == nwords - 1 && (nrows & 63)) act &= (1ULL << (nrows & 63)) - 1;
-        if (act == 0) {
-            if (lane == 0) tbits[w] = 0;
-            continue;
+    const uint64_t tail = (nrows & 63) ? ((1ULL << (nrows & 63)) - 1) : ~0ULL;
+    long long cnt = 0;
+    for (int64_t w0 = wave * PULL_U; w0 < nwords; w0 += nwaves * PULL_U) {
+        const int64_t wl = w0 + (lane & (PULL_U - 1));
+        uint64_t mine = ~0ULL;
+        if (mbits) mine = wl < nwords ? (mcomp ? ~mbits[wl] : mbits[wl]) : 0;
+        if (wl == nwords - 1) mine &= tail;
+        if (wl >= nwords) mine = 0;
+        bool live[PULL_U], found[PULL_U];
+        int64_t p[PULL_U], p1[PULL_U];
+#pragma unroll
+        for (int u = 0; u < PULL_U; u++) {
+            live[u] = (__shfl(mine, u, 64) >> lane) & 1ULL;
+            found[u] = false;
+            p[u] = p1[u] = 0;
+            if (live[u]) {
+                const int64_t r = ((w0 + u) << 6) + lane;
+                p[u] = rowptr[r];
+                p1[u] = rowptr[r + 1];
+            }
         }
-        const int64_t r = (w << 6) + lane;
-        const bool live = (act >> lane) & 1ULL;
-        int64_t p = 0, p1 = 0;
-        if (live) {
-            p = rowptr[r];
-            p1 = rowptr[r + 1];
-        }
-        bool found = false;
         for (int it = 0; it < 4; it++) {
-            const bool go = live && !found && p < p1;
-            if (!__ballot(go)) break;
-            if (go) {
-                const int k0 = colidx[p];
-                const int k1 = (p + 1 < p1) ? colidx[p + 1] : k0;
-                found = (gb_bit(ubits, k0) + gb_bit(ubits, k1)) != 0;
-                p += 2;
+            bool go[PULL_U], any = false;
+#pragma unroll
+            for (int u = 0; u < PULL_U; u++) {
+                go[u] = live[u] && !found[u] && p[u] < p1[u];
+                any = any || go[u];
+            }
+            if (!__ballot(any)) break;
+            int k0[PULL_U], k1[PULL_U];
+#pragma unroll
+            for (int u = 0; u < PULL_U; u++) {
+                if (go[u]) {
+                    k0[u] = colidx[p[u]];
+                    k1[u] = (p[u] + 1 < p1[u]) ? colidx[p[u] + 1] : k0[u];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < PULL_U; u++) {
+                if (go[u]) {
+                    found[u] = (gb_bit(ubits, k0[u]) + gb_bit(ubits, k1[u])) != 0;
+                    p[u] += 2;
+                }
             }
         }
-        unsigned long long pend = __ballot(live && !found && p < p1);
-        while (pend) {
-            const int l = __ffsll(pend) - 1;
-            pend &= pend - 1;
-            const int64_t q0 = __shfl(p, l, 64), q1 = __shfl(p1, l, 64);
-            bool f = false;
-            for (int64_t q = q0 + lane; q < q1; q += 256) {
-                int j[4];
 #pragma unroll
-                for (int u = 0; u < 4; u++) j[u] = (q + 64 * u < q1) ? colidx[q + 64 * u] : -1;
-#pragma unroll
-                for (int u = 0; u < 4; u++) f = f || (j[u] >= 0 && gb_bit(ubits, j[u]));
-                if (__ballot(f)) break;
+        for (int u = 0; u < PULL_U; u++) {
+            // rows still open: eight at a time, eight lanes per row
+            unsigned long long pend = __ballot(live[u] && !found[u] && p[u] < p1[u]);
+            unsigned long long hit = 0;
+            const int g = lane >> 3, gl = lane & 7;
+            while (pend) {
+                const unsigned long long round = pend;
+                unsigned long long t = pend;
+                int mine = -1;
+                for (int i = 0; i < 8 && t; i++) {
+                    const int b = __ffsll(t) - 1;
+                    t &= t - 1;
+                    if (i == g) mine = b;
+                }
+                pend = t;
+                const int src = mine < 0 ? 0 : mine;
+                const int64_t q0 = __shfl(p[u], src, 64), q1 = __shfl(p1[u], src, 64);
+                bool f = false;
+                if (mine >= 0) {
+                    for (int64_t q = q0 + gl; q < q1; q += 8) {
+                        f = gb_bit(ubits, colidx[q]);
+                        if ((__ballot(f) >> (g * 8)) & 0xFFULL) break;
+                    }
+                }
+                const unsigned long long fb = __ballot(f);
+                t = round;
+                for (int i = 0; i < 8 && t; i++) {
+                    const int b = __ffsll(t) - 1;
+                    t &= t - 1;
+                    if ((fb >> (i * 8)) & 0xFFULL) hit |= 1ULL << b;
+                }
             }
-            if (__ballot(f) && lane == l) found = true;
-        }
-        const unsigned long long word = __ballot(found);
-        if (lane == 0) {
-            tbits[w] = word;
-            cnt += __popcll(word);
+            if ((hit >> lane) & 1ULL) found[u] = true;
+            const unsigned long long word = __ballot(found[u]);
+            if (lane == 0 && w0 + u < nwords) {
+                tbits[w0 + u] = word;
+                cnt += __popcll(word);
+            }
         }
     }
-    gb_block_add(cnt, tcount);
+    return cnt;
+}
+
+// One launch does the chosen direction (dst[ST_PUSH], set by k_dir_prep; dst
+// null: pull only).  Counts the output bits into *tcount.
+__global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
+    int64_t nrows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ colidx,
+    int64_t nwords_u, const uint64_t *__restrict__ ubits, const int64_t *__restrict__ prow,
+    const int32_t *__restrict__ pcol, const int32_t *__restrict__ hubs, int64_t nhubs, int64_t H,
+    const uint64_t *__restrict__ mbits, bool mcomp, uint64_t *__restrict__ tbits,
+    unsigned long long *__restrict__ tcount, unsigned long long *__restrict__ gst,
+    const unsigned long long *__restrict__ dst) {
+    long long cnt;
+    if (dst && dst[ST_PUSH])
+        cnt = gb_push_phase(nwords_u, ubits, prow, pcol, hubs, nhubs, H, mbits, mcomp,
+                            (unsigned long long *)tbits);
+    else
+        cnt = gb_pull_iso_phase(nrows, rowptr, colidx, ubits, mbits, mcomp, tbits);
+    gb_grid_add(cnt, tcount, gst);
+}
+
+// hub-chunk table of a CSR: pieces per row, then (row, piece) pairs
+__global__ void k_hub_count(const int64_t *__restrict__ rowptr, int64_t n, int64_t H, int64_t *__restrict__ cnt) {
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t d = rowptr[r + 1] - rowptr[r];
+        cnt[r] = d > H ? (d + H - 1) / H : 0;
+    }
+}
+__global__ void k_hub_fill(const int64_t *__restrict__ cnt, const int64_t *__restrict__ off, int64_t n,
+                           int32_t *__restrict__ tab) {
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t c = cnt[r], o = off[r];
+        for (int64_t i = 0; i < c; i++) {
+            tab[2 * (o + i)] = (int32_t)r;
+            tab[2 * (o + i) + 1] = (int32_t)i;
+        }
+    }
+}
+
+void gb_view_hubs(gb_csr_view &v, GB_Obj *A, int orient, int64_t H) {
+    if (A->kind != GB_KIND_MATRIX) return;
+    if (!A->hub_tab[orient] || A->hub_H[orient] != H) {
+        gb_free(A->hub_tab[orient]);
+        A->hub_tab[orient] = nullptr;
+        const int64_t n = v.nrows;
+        gb_scratch s;
+        int64_t *cnt = s.get<int64_t>(n + 1);
+        int64_t *off = s.get<int64_t>(n + 1);
+        const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
+        hipLaunchKernelGGL(k_hub_count, dim3(g), dim3(256), 0, gb_stream(), v.rowptr, n, H, cnt);
+        GB_LAUNCH_CHECK();
+        gb_exclusive_scan_i64(cnt, off, n);
+        const int64_t total = gb_read_i64(off + n);
+        A->hub_tab[orient] = gb_malloc_n<int32_t>(2 * total + 2);
+        hipLaunchKernelGGL(k_hub_fill, dim3(g), dim3(256), 0, gb_stream(), cnt, off, n, A->hub_tab[orient]);
+        GB_LAUNCH_CHECK();
+        A->hub_n[orient] = total;
+        A->hub_H[orient] = H;
+    }
+    v.hubs = A->hub_tab[orient];
+    v.nhubs = A->hub_n[orient];
+    v.hub_H = H;
 }
 
 // constant value of an iso result: mult(a0, u0) (positional ops are never iso)
@@ -350,17 +450,7 @@ static bool idempotent_monoid(int m) {
            m == GBAMD_MON_LAND || m == GBAMD_MON_BOR || m == GBAMD_MON_BAND;
 }
 
-// the persistent direction state (see k_dir_prep), allocated and zeroed once
-static std::mutex g_dir_mu;
-static unsigned long long *gb_dir_state() {
-    static unsigned long long *st = nullptr;
-    if (!st) {
-        GB_HIP(hipMalloc(&st, ST_WORDS * sizeof(unsigned long long)));
-        GB_HIP(hipMemset(st, 0, ST_WORDS * sizeof(unsigned long long)));
-        GB_HIP(hipDeviceSynchronize());
-    }
-    return st;
-}
+static std::mutex g_dir_mu;  // keeps the prep/push/pull launches of one call adjacent
 
 bool gb_spmv_result_iso(GrB_Semiring sr, bool a_iso, bool u_iso, bool flip) {
     gb_sr_info info = gb_sr_describe(sr);
@@ -394,62 +484,59 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
     }
 
     const int64_t dir_knob = gb_knob("spmv_direction");  // 0 auto, 1 pull only, 2 push only
-    const bool can_push = iso && Apush && Apush->nrows == u.n && dir_knob != 1;
+    const bool can_push = iso && Apush && Apush->nrows == u.n && Apush->hubs && dir_knob != 1;
     int64_t alpha = gb_knob("push_alpha");
     if (alpha <= 0) alpha = 14;
-    int64_t H = gb_knob("push_heavy");
-    if (H <= 0) H = 2048;
     const int64_t nw = gb_words(n);
-    const unsigned iso_grid = (unsigned)std::min<int64_t>((nw + 3) / 4, 8192);
+    unsigned long long *gst = gb_device_state();
+    unsigned long long *dst = gst + GB_DIR_STATE_OFFSET;
 
     gb_dispatch_sr(info, [&](auto srf, auto x, auto z) {
         using SRT = decltype(srf);
         using X = decltype(x);
         using Z = decltype(z);
-        if (can_push) {
-            // prep -> push -> pull, one direction doing the work; the other returns at once
-            std::lock_guard<std::mutex> lk(g_dir_mu);  // keeps the three launches adjacent
-            unsigned long long *state = gb_dir_state();
+        if (iso) {
             const int64_t uw = gb_words(u.n);
-            unsigned long long *part = s.get<unsigned long long>(PREP_BLOCKS);
-            int64_t *chunks = s.get<int64_t>(2 * (2 * (Apush->nvals / H) + 2));
-            gb_dir_rule rule{mask.count, mask.comp, n, A.nvals, alpha, dir_knob == 2};
-            if (flip)
-                hipLaunchKernelGGL((k_dir_prep<SRT, X, Z, true>), dim3(PREP_BLOCKS), dim3(SPMV_BLOCK), 0, gb_stream(),
-                                   srf, u.bits, uw, Apush->rowptr, H, chunks, part, state, T.bits, nw,
-                                   (unsigned long long *)T.d_nvals, (const X *)av, (const X *)uv, (Z *)T.dense,
-                                   rule);
-            else
-                hipLaunchKernelGGL((k_dir_prep<SRT, X, Z, false>), dim3(PREP_BLOCKS), dim3(SPMV_BLOCK), 0,
-                                   gb_stream(), srf, u.bits, uw, Apush->rowptr, H, chunks, part, state, T.bits, nw,
-                                   (unsigned long long *)T.d_nvals, (const X *)av, (const X *)uv, (Z *)T.dense,
-                                   rule);
-            GB_LAUNCH_CHECK();
-            const unsigned pgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((uw + 3) / 4, 2048));
-            hipLaunchKernelGGL(k_push, dim3(pgrid), dim3(SPMV_BLOCK), 0, gb_stream(), uw, u.bits, Apush->rowptr,
-                               Apush->colidx, mask.bits, mask.comp, (unsigned long long *)T.bits,
-                               (unsigned long long *)T.d_nvals, chunks, state, H);
-            GB_LAUNCH_CHECK();
-            hipLaunchKernelGGL(k_pull_iso, dim3(iso_grid), dim3(SPMV_BLOCK), 0, gb_stream(), n, A.rowptr, A.colidx,
-                               u.bits, mask.bits, mask.comp, T.bits, (unsigned long long *)T.d_nvals, state);
+            int64_t units = (nw + PULL_U - 1) / PULL_U;  // waves the pull wants
+            std::unique_lock<std::mutex> lk(g_dir_mu, std::defer_lock);
+            if (can_push) {
+                // prep (frontier edges -> direction, zeroed output, iso value), then one work launch
+                lk.lock();
+                units = std::max<int64_t>(units, Apush->nhubs + uw);
+                gb_dir_rule rule{mask.count, mask.comp, n, A.nvals, alpha, dir_knob == 2};
+                const unsigned prep_grid =
+                    (unsigned)std::max<int64_t>(1, std::min<int64_t>((uw + 4 * PULL_U - 1) / (4 * PULL_U), 1024));
+                if (flip)
+                    hipLaunchKernelGGL((k_dir_prep<SRT, X, Z, true>), dim3(prep_grid), dim3(SPMV_BLOCK), 0,
+                                       gb_stream(), srf, u.bits, uw, Apush->rowptr, gst, dst, T.bits, nw,
+                                       (unsigned long long *)T.d_nvals, (const X *)av, (const X *)uv, (Z *)T.dense,
+                                       rule);
+                else
+                    hipLaunchKernelGGL((k_dir_prep<SRT, X, Z, false>), dim3(prep_grid), dim3(SPMV_BLOCK), 0,
+                                       gb_stream(), srf, u.bits, uw, Apush->rowptr, gst, dst, T.bits, nw,
+                                       (unsigned long long *)T.d_nvals, (const X *)av, (const X *)uv, (Z *)T.dense,
+                                       rule);
+                GB_LAUNCH_CHECK();
+            } else {
+                gb_memset(T.d_nvals, 0, sizeof(int64_t));
+                if (flip)
+                    hipLaunchKernelGGL((k_iso_value<SRT, X, Z, true>), dim3(1), dim3(1), 0, gb_stream(), srf,
+                                       (const X *)av, (const X *)uv, (Z *)T.dense);
+                else
+                    hipLaunchKernelGGL((k_iso_value<SRT, X, Z, false>), dim3(1), dim3(1), 0, gb_stream(), srf,
+                                       (const X *)av, (const X *)uv, (Z *)T.dense);
+                GB_LAUNCH_CHECK();
+            }
+            const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 3) / 4, 4096));
+            hipLaunchKernelGGL(k_iso_work, dim3(grid), dim3(SPMV_BLOCK), 0, gb_stream(), n, A.rowptr, A.colidx, uw,
+                               u.bits, can_push ? Apush->rowptr : nullptr, can_push ? Apush->colidx : nullptr,
+                               can_push ? Apush->hubs : nullptr, can_push ? Apush->nhubs : 0,
+                               can_push ? Apush->hub_H : 1, mask.bits, mask.comp, T.bits,
+                               (unsigned long long *)T.d_nvals, gst, can_push ? dst : nullptr);
             GB_LAUNCH_CHECK();
             return;
         }
         gb_memset(T.d_nvals, 0, sizeof(int64_t));
-        if (iso) {
-            hipLaunchKernelGGL(k_pull_iso, dim3(iso_grid), dim3(SPMV_BLOCK), 0, gb_stream(), n, A.rowptr, A.colidx,
-                               u.bits, mask.bits, mask.comp, T.bits, (unsigned long long *)T.d_nvals,
-                               (unsigned long long *)nullptr);
-            GB_LAUNCH_CHECK();
-            if (flip)
-                hipLaunchKernelGGL((k_iso_value<SRT, X, Z, true>), dim3(1), dim3(1), 0, gb_stream(), srf,
-                                   (const X *)av, (const X *)uv, (Z *)T.dense);
-            else
-                hipLaunchKernelGGL((k_iso_value<SRT, X, Z, false>), dim3(1), dim3(1), 0, gb_stream(), srf,
-                                   (const X *)av, (const X *)uv, (Z *)T.dense);
-            GB_LAUNCH_CHECK();
-            return;
-        }
         // general semiring: G lanes per row, G from the average row length
         const int64_t avg = (A.nvals + n - 1) / n;
         int lg = 0;
@@ -460,11 +547,11 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
         if (flip)
             hipLaunchKernelGGL((k_spmv_pull<SRT, X, Z, true>), dim3(grid), dim3(SPMV_BLOCK), 0, gb_stream(), srf, n,
                                A.rowptr, A.colidx, (const X *)av, A.iso, u.bits, (const X *)uv, u.iso, mask.bits,
-                               mask.comp, lg, T.bits, (Z *)T.dense, (unsigned long long *)T.d_nvals);
+                               mask.comp, lg, T.bits, (Z *)T.dense, (unsigned long long *)T.d_nvals, gst);
         else
             hipLaunchKernelGGL((k_spmv_pull<SRT, X, Z, false>), dim3(grid), dim3(SPMV_BLOCK), 0, gb_stream(), srf, n,
                                A.rowptr, A.colidx, (const X *)av, A.iso, u.bits, (const X *)uv, u.iso, mask.bits,
-                               mask.comp, lg, T.bits, (Z *)T.dense, (unsigned long long *)T.d_nvals);
+                               mask.comp, lg, T.bits, (Z *)T.dense, (unsigned long long *)T.d_nvals, gst);
         GB_LAUNCH_CHECK();
     });
 }

@@ -112,6 +112,11 @@ void gb_drop_transpose(GB_Obj *A) {
     A->t_colidx = nullptr;
     A->t_vals = nullptr;
     A->t_valid = false;
+    for (int o = 0; o < 2; o++) {
+        gb_free(A->hub_tab[o]);
+        A->hub_tab[o] = nullptr;
+        A->hub_n[o] = A->hub_H[o] = 0;
+    }
 }
 
 void gb_obj_free_storage(GB_Obj *A) {

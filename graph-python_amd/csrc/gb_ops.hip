@@ -60,6 +60,8 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
         gb_spmv_result_iso(sr, A->iso, uv.iso, vxm)) {
         if (use_csc) gb_get_csr(pv, A);
         else gb_get_csc(pv, A);
+        int64_t H = gb_knob("push_heavy");
+        gb_view_hubs(pv, A, use_csc ? 0 : 1, H > 0 ? H : 512);
         push = &pv;
     }
     gb_vec_result T;
@@ -100,7 +102,8 @@ static void do_mxm(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, GrB_Semiring sr, GB
 template <class X, class Z>
 __global__ void k_ewise_vec(int64_t n, int op, bool add, const uint64_t *__restrict__ ub, const X *__restrict__ ux,
                             bool u_iso, const uint64_t *__restrict__ vb, const X *__restrict__ vx, bool v_iso,
-                            uint64_t *__restrict__ ob, Z *__restrict__ oz, unsigned long long *__restrict__ cnt) {
+                            uint64_t *__restrict__ ob, Z *__restrict__ oz, unsigned long long *__restrict__ cnt,
+                            unsigned long long *__restrict__ gst) {
     unsigned long long mine = 0;
     for (int64_t base = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) & ~63LL; base < n;
          base += (int64_t)gridDim.x * blockDim.x) {
@@ -118,7 +121,7 @@ __global__ void k_ewise_vec(int64_t n, int op, bool add, const uint64_t *__restr
             mine += __popcll(w);
         }
     }
-    gb_block_add(mine, cnt);
+    gb_grid_add((long long)mine, cnt, gst);
 }
 
 template <class X, class Z, bool FILL>
@@ -196,7 +199,7 @@ static void do_ewise(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, GrB_BinaryOp op, 
             if (n)
                 hipLaunchKernelGGL((k_ewise_vec<X, Z>), dim3(ops_grid(n, 1024)), dim3(OPS_BLOCK), 0, gb_stream(), n,
                                    op->opcode, add, ua.bits, (const X *)xa, ua.iso, ub.bits, (const X *)xb, ub.iso,
-                                   T.bits, (Z *)T.dense, (unsigned long long *)T.d_nvals);
+                                   T.bits, (Z *)T.dense, (unsigned long long *)T.d_nvals, gb_device_state());
         });
         GB_LAUNCH_CHECK();
         gb_writeback_vector(C, T, M, d, accum, false);
@@ -416,7 +419,8 @@ static GrB_BinaryOp second_of(int code) {
 template <class T>
 __global__ __launch_bounds__(OPS_BLOCK) void k_assign_all_scalar(
     int64_t n, uint64_t *__restrict__ cbits, T *__restrict__ cvals, const uint64_t *__restrict__ mbits, bool mcomp,
-    const void *miso, int miso_code, bool replace, T x, unsigned long long *__restrict__ count) {
+    const void *miso, int miso_code, bool replace, T x, unsigned long long *__restrict__ count,
+    unsigned long long *__restrict__ gst) {
     // value mask over an iso vector: the mask is its structure if the value is true, else empty
     const bool iso_true = miso ? gb_dyn_nonzero(miso, miso_code) : true;
     long long delta = 0;  // change of nvals(C); added to the count C already holds
@@ -439,7 +443,7 @@ __global__ __launch_bounds__(OPS_BLOCK) void k_assign_all_scalar(
             delta += (long long)__popcll(word) - (long long)__popcll(cword);
         }
     }
-    gb_block_add((unsigned long long)delta, count);
+    gb_grid_add(delta, count, gst);
 }
 
 // w<M>(:) = x, M a plain (non-complemented) mask, no replace: a thread per
@@ -449,7 +453,8 @@ __global__ __launch_bounds__(OPS_BLOCK) void k_assign_mask_words(int64_t nwords,
                                                                  T *__restrict__ cvals,
                                                                  const uint64_t *__restrict__ mbits, const void *miso,
                                                                  int miso_code, T x,
-                                                                 unsigned long long *__restrict__ count) {
+                                                                 unsigned long long *__restrict__ count,
+                                                                 unsigned long long *__restrict__ gst) {
     const bool iso_true = miso ? gb_dyn_nonzero(miso, miso_code) : true;
     long long delta = 0;
     if (iso_true) {
@@ -467,7 +472,7 @@ __global__ __launch_bounds__(OPS_BLOCK) void k_assign_mask_words(int64_t nwords,
             }
         }
     }
-    gb_block_add((unsigned long long)delta, count);
+    gb_grid_add(delta, count, gst);
 }
 
 static bool assign_all_scalar_fast(GB_Obj *w, GB_Obj *mask, const char *xc, const gb_desc &d) {
@@ -516,11 +521,11 @@ static bool assign_all_scalar_fast(GB_Obj *w, GB_Obj *mask, const char *xc, cons
             hipLaunchKernelGGL(k_assign_mask_words<T>,
                                dim3((unsigned)std::min<int64_t>((gb_words(n) + OPS_BLOCK - 1) / OPS_BLOCK, 1024)),
                                dim3(OPS_BLOCK), 0, gb_stream(), gb_words(n), w->bits, (T *)w->dense, m.bits, m.iso_val,
-                               m.iso_code, xv, (unsigned long long *)w->d_nvals);
+                               m.iso_code, xv, (unsigned long long *)w->d_nvals, gb_device_state());
         else if (n)
             hipLaunchKernelGGL(k_assign_all_scalar<T>, dim3(grid), dim3(OPS_BLOCK), 0, gb_stream(), n, w->bits,
                                (T *)w->dense, m.bits, m.comp, m.iso_val, m.iso_code, d.replace, xv,
-                               (unsigned long long *)w->d_nvals);
+                               (unsigned long long *)w->d_nvals, gb_device_state());
     });
     GB_LAUNCH_CHECK();
     w->nvals_valid = false;

@@ -154,7 +154,7 @@ __global__ __launch_bounds__(WB_BLOCK) void k_vec_merge(
     int64_t n, const uint64_t *__restrict__ cbits, const CT *__restrict__ cvals, bool c_iso,
     const uint64_t *__restrict__ tbits, const CT *__restrict__ tvals, bool t_iso, const uint64_t *__restrict__ mbits,
     bool mcomp, bool replace, int accum, uint64_t *__restrict__ obits, CT *__restrict__ ovals,
-    unsigned long long *__restrict__ count) {
+    unsigned long long *__restrict__ count, unsigned long long *__restrict__ gst) {
     unsigned long long mine = 0;
     // 64 consecutive elements per wave -> one output word per wave
     for (int64_t base = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) & ~63LL; base < n;
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(WB_BLOCK) void k_vec_merge(
             mine += __popcll(word);
         }
     }
-    gb_block_add(mine, count);
+    gb_grid_add((long long)mine, count, gst);
 }
 
 static void cast_vec_result(gb_vec_result &T, int code) {
@@ -252,7 +252,7 @@ void gb_writeback_vector(GB_Obj *C, gb_vec_result &T, GB_Obj *M, const gb_desc &
             hipLaunchKernelGGL(k_vec_merge<W>, dim3(wb_grid(n, 1024)), dim3(WB_BLOCK), 0, gb_stream(), n, cv.bits,
                                (const W *)cvals, c_iso, T.bits, (const W *)T.dense, T.iso, mask.bits, mask.comp,
                                d.replace, accum ? accum->opcode : -1, obits, (W *)ovals,
-                               (unsigned long long *)cnt);
+                               (unsigned long long *)cnt, gb_device_state());
         });
         GB_LAUNCH_CHECK();
     }
