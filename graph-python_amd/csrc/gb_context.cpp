@@ -5,6 +5,7 @@
 // core/descriptor.py:92-156.)
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <unordered_map>
@@ -57,9 +58,78 @@ void gb_require_init() {
     if (!g_init) gb_do_init();  // lazy init, like python-graphblas's auto-init
 }
 
+static std::atomic<uint64_t> g_epoch{1};
+uint64_t gb_epoch() { return g_epoch.load(std::memory_order_relaxed); }
+
 hipStream_t gb_stream() {
     gb_require_init();
+    g_epoch.fetch_add(1, std::memory_order_relaxed);  // every caller is about to enqueue work
     return g_user_stream_set ? g_user_stream : g_own_stream;
+}
+hipStream_t gb_stream_peek() {
+    gb_require_init();
+    return g_user_stream_set ? g_user_stream : g_own_stream;
+}
+
+// ---- host mailboxes (see gb_internal.h)
+namespace {
+std::mutex g_slot_mu;
+std::vector<gb_host_slot *> g_slot_free;
+std::vector<std::pair<gb_host_slot *, gb_host_slot *>> g_slot_slabs;  // (host base, device base)
+std::atomic<uint64_t> g_pub_seq{0};
+const int kSlotsPerSlab = 1024;
+}  // namespace
+
+gb_host_slot *gb_host_slot_alloc() {
+    std::lock_guard<std::mutex> lk(g_slot_mu);
+    if (g_slot_free.empty()) {
+        gb_require_init();
+        gb_host_slot *h = nullptr, *d = nullptr;
+        GB_HIP(hipHostMalloc((void **)&h, kSlotsPerSlab * sizeof(gb_host_slot),
+                             hipHostMallocCoherent | hipHostMallocMapped));
+        GB_HIP(hipHostGetDevicePointer((void **)&d, h, 0));
+        memset(h, 0, kSlotsPerSlab * sizeof(gb_host_slot));
+        g_slot_slabs.push_back({h, d});
+        for (int i = kSlotsPerSlab - 1; i >= 0; i--) g_slot_free.push_back(h + i);
+    }
+    gb_host_slot *s = g_slot_free.back();
+    g_slot_free.pop_back();
+    return s;
+}
+
+void gb_host_slot_release(gb_host_slot *s) {
+    if (!s) return;
+    std::lock_guard<std::mutex> lk(g_slot_mu);
+    g_slot_free.push_back(s);
+}
+
+gb_host_slot *gb_host_slot_device(gb_host_slot *s) {
+    std::lock_guard<std::mutex> lk(g_slot_mu);
+    for (auto &sl : g_slot_slabs)
+        if (s >= sl.first && s < sl.first + kSlotsPerSlab) return sl.second + (s - sl.first);
+    return nullptr;
+}
+
+uint64_t gb_next_pub_seq() { return g_pub_seq.fetch_add(1, std::memory_order_relaxed) + 1; }
+
+bool gb_host_slot_wait(gb_host_slot *s, uint64_t seq, int64_t *value) {
+    for (uint64_t i = 1;; i++) {
+        if ((uint64_t)__atomic_load_n(&s->seq, __ATOMIC_ACQUIRE) == seq) {
+            *value = __atomic_load_n(&s->value, __ATOMIC_RELAXED);
+            return true;
+        }
+        if ((i & 1023) == 0) {
+            hipError_t q = hipStreamQuery(gb_stream_peek());
+            if (q != hipErrorNotReady) {  // drained (or failed): one last look
+                if ((uint64_t)__atomic_load_n(&s->seq, __ATOMIC_ACQUIRE) == seq) {
+                    *value = __atomic_load_n(&s->value, __ATOMIC_RELAXED);
+                    return true;
+                }
+                return false;
+            }
+        }
+        __builtin_ia32_pause();
+    }
 }
 
 void gb_sync() { GB_HIP(hipStreamSynchronize(gb_stream())); }

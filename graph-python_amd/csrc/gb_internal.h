@@ -87,6 +87,10 @@ struct GB_Matrix_opaque {
     void *dense;         // [n] or [1] when iso
     int64_t *d_nvals;    // device counter kept current by every writer
     bool nvals_valid;    // host copy in `nvals` is current
+    // host-visible copy of d_nvals published by the kernel that produced it
+    // (valid while pub_epoch == gb_epoch(): nothing enqueued since)
+    struct gb_host_slot *pub;
+    uint64_t pub_seq, pub_epoch;
     std::string err;
 };
 typedef GB_Matrix_opaque GB_Obj;
@@ -133,7 +137,26 @@ void gb_require_init();
 void gb_sync();
 int64_t gb_knob(const char *key);
 // persistent zeroed device words (layout: gb_state.h), allocated on first use
-unsigned long long *gb_device_state();  // tuning knobs (0 = auto)
+unsigned long long *gb_device_state();
+
+// Host-visible mailboxes in pinned coherent memory: a kernel publishes a
+// device count with a sequence number (system-scope store); the host spins on
+// it instead of a copy + stream synchronisation.
+struct gb_host_slot {
+    long long seq;
+    long long value;
+    long long pad[6];
+};
+gb_host_slot *gb_host_slot_alloc();
+void gb_host_slot_release(gb_host_slot *s);
+gb_host_slot *gb_host_slot_device(gb_host_slot *s);  // device address of the same slot
+uint64_t gb_next_pub_seq();
+// count of work enqueued through gb_stream() (a published value is current only
+// while no later work has been enqueued)
+uint64_t gb_epoch();
+hipStream_t gb_stream_peek();  // the library stream, without counting an enqueue
+// wait for slot->seq == seq; false if the stream drained without it (caller falls back)
+bool gb_host_slot_wait(gb_host_slot *s, uint64_t seq, int64_t *value);  // tuning knobs (0 = auto)
 
 // device memory (stream-ordered pool on the library stream)
 void *gb_malloc(size_t bytes);        // throws GrB_OUT_OF_MEMORY
@@ -271,6 +294,9 @@ struct gb_vec_result {  // bitmap, type code ztype
     bool iso = false;
     int tcode = 0;
     int64_t *d_nvals = nullptr;
+    gb_host_slot *pub = nullptr;  // if set, the producing kernel publishes nvals here
+    uint64_t pub_seq = 0;
+    bool published = false;       // set by the producer when it did publish
 };
 struct gb_mat_result {  // CSR
     int64_t nrows = 0, ncols = 0, nvals = 0;
@@ -283,7 +309,8 @@ struct gb_mat_result {  // CSR
 };
 
 // C<M,replace> = C accum T  (takes ownership of T's buffers)
-void gb_writeback_vector(GB_Obj *C, gb_vec_result &T, GB_Obj *M, const gb_desc &d,
+// returns true when T was installed into C as is (no merge)
+bool gb_writeback_vector(GB_Obj *C, gb_vec_result &T, GB_Obj *M, const gb_desc &d,
                          GrB_BinaryOp accum, bool t_within_mask);
 void gb_writeback_matrix(GB_Obj *C, gb_mat_result &T, GB_Obj *M, const gb_desc &d,
                          GrB_BinaryOp accum);

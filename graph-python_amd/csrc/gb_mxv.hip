@@ -139,21 +139,30 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_dir_prep(
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     long long mf = 0;
-    for (int64_t w0 = wave * PULL_U; w0 < nwords_u; w0 += nwaves * PULL_U) {
-        const int64_t wl = w0 + (lane & (PULL_U - 1));
+    // 16 frontier words per wave step (lanes 0-15 load them); the non-zero ones
+    // are expanded one lane per bit, four words at a time
+    for (int64_t base = wave * 16; base < nwords_u; base += nwaves * 16) {
+        const int64_t wl = base + (lane & 15);
         const uint64_t mine = wl < nwords_u ? ubits[wl] : 0;
-        int64_t deg[PULL_U];
+        unsigned long long nz = __ballot(mine != 0) & 0xFFFFULL;
+        while (nz) {
+            int64_t deg[4];
 #pragma unroll
-        for (int u = 0; u < PULL_U; u++) {
-            const uint64_t word = __shfl(mine, u, 64);
-            deg[u] = 0;
-            if ((word >> lane) & 1ULL) {
-                const int64_t k = ((w0 + u) << 6) + lane;
-                deg[u] = prow[k + 1] - prow[k];
+            for (int u = 0; u < 4; u++) {
+                deg[u] = 0;
+                if (nz) {
+                    const int l = __ffsll(nz) - 1;
+                    nz &= nz - 1;
+                    const uint64_t word = __shfl(mine, l, 64);
+                    if ((word >> lane) & 1ULL) {
+                        const int64_t k = ((base + l) << 6) + lane;
+                        deg[u] = prow[k + 1] - prow[k];
+                    }
+                }
             }
-        }
 #pragma unroll
-        for (int u = 0; u < PULL_U; u++) mf += deg[u];
+            for (int u = 0; u < 4; u++) mf += deg[u];
+        }
     }
     const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     for (int64_t w = tid; w < nwords_out; w += (int64_t)gridDim.x * blockDim.x) tbits[w] = 0;
@@ -202,26 +211,103 @@ __device__ __forceinline__ long long gb_push_targets(const int32_t (&j)[4], bool
     return added;
 }
 
-// Push (top-down).  Units [0, nhubs) are the matrix's hub chunks (rows longer
-// than H cut into H-edge pieces, a static table): a wave takes a chunk if its
-// row is in the frontier, 256 edges a step.  Then one unit per frontier word:
-// the rows of its frontier vertices (at most H edges each) are concatenated
-// and spread over the wave's lanes, 256 edges a step (wave prefix sum of the
-// row lengths; a lane finds the row of its edge by binary search over it).
+// ------------------------------------------------ wave-level segment lists (LDS)
+// A wave gathers up to WL_MAX row segments (start, length) into its own LDS
+// area, takes a prefix sum of the lengths and then walks the concatenated
+// edges 256 at a time, four independent loads per lane; a lane finds the
+// segment of its edge by binary search over the prefix.  This keeps every lane
+// busy whatever the mix of row lengths (no lane-per-row tail, no wave per row).
+#define WL_MAX 256
+#define WAVES_PER_BLOCK (SPMV_BLOCK / 64)
+struct gb_wlist {
+    int64_t p[WL_MAX];    // next edge position of the segment
+    int32_t rem[WL_MAX];  // edges left in the row
+    int32_t pref[WL_MAX]; // inclusive prefix of this round's lengths
+    int16_t id[WL_MAX];   // u * 64 + lane of the row (pull)
+    int8_t hit[WL_MAX];   // a k present in u was found this round
+};
+
+__device__ __forceinline__ void gb_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// this round takes min(rem[i], cap) edges of segment i; hit[i] = 0; pref = inclusive
+// prefix of the taken lengths; returns the total
+__device__ __forceinline__ int gb_wlist_round(gb_wlist &L, int n, int cap, int lane) {
+    int v[4], sum = 0;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const int i = lane * 4 + t;
+        v[t] = 0;
+        if (i < n) {
+            v[t] = L.rem[i] < cap ? L.rem[i] : cap;
+            L.hit[i] = 0;
+        }
+        sum += v[t];
+    }
+    int incl = sum;
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    int run = incl - sum;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const int i = lane * 4 + t;
+        run += v[t];
+        if (i < n) L.pref[i] = run;
+    }
+    gb_wave_sync();
+    return __shfl(incl, 63, 64);
+}
+
+// start of segment i's edges in the concatenated stream
+__device__ __forceinline__ int gb_wlist_start(const gb_wlist &L, int i) { return i ? L.pref[i - 1] : 0; }
+
+// segment of concatenated edge e: first i with pref[i] > e (n <= WL_MAX)
+__device__ __forceinline__ int gb_wlist_find(const gb_wlist &L, int n, int e) {
+    int lo = 0;
+#pragma unroll
+    for (int st = WL_MAX / 2; st > 0; st >>= 1)
+        if (lo + st <= n && L.pref[lo + st - 1] <= e) lo += st;
+    return lo;
+}
+
+// Push (top-down).  First the matrix's hub chunks (rows longer than H cut into
+// H-edge pieces, a static table; a wave tests 16 strided entries against the
+// frontier at once and expands the hits, 256 edges a step).  Then the frontier
+// words, 4 per wave step: the rows of their frontier vertices (at most H edges
+// each) go into the wave's segment list and are walked as one edge stream.
 __device__ __forceinline__ long long gb_push_phase(int64_t nwords_u, const uint64_t *__restrict__ ubits,
                                                   const int64_t *__restrict__ prow, const int32_t *__restrict__ pcol,
                                                   const int32_t *__restrict__ hubs, int64_t nhubs, int64_t H,
                                                   const uint64_t *__restrict__ mbits, bool mcomp,
-                                                  unsigned long long *__restrict__ tbits) {
+                                                  unsigned long long *__restrict__ tbits, gb_wlist &L) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const unsigned long long lt = (1ULL << lane) - 1;
     long long added = 0;
-    for (int64_t unit = wave; unit < nhubs + nwords_u; unit += nwaves) {
-        if (unit < nhubs) {
-            const int64_t k = hubs[2 * unit], c = hubs[2 * unit + 1];
-            if (!gb_bit(ubits, k)) continue;
-            const int64_t p0 = prow[k] + c * H, pe = prow[k + 1];
+    // hub chunks: lane l of wave w tests table entry w + l * nwaves (a hub's
+    // consecutive chunks land on different waves); hits are expanded in turn
+    for (int64_t base = wave; base < nhubs; base += nwaves * 16) {
+        const int64_t h = base + (int64_t)lane * nwaves;
+        int k = 0, cc = 0;
+        bool act = false;
+        if (lane < 16 && h < nhubs) {
+            k = hubs[2 * h];
+            cc = hubs[2 * h + 1];
+            act = gb_bit(ubits, k);
+        }
+        unsigned long long b = __ballot(act);
+        while (b) {
+            const int l = __ffsll(b) - 1;
+            b &= b - 1;
+            const int64_t kk = __shfl(k, l, 64);
+            const int64_t c = __shfl(cc, l, 64);
+            const int64_t p0 = prow[kk] + c * H, pe = prow[kk + 1];
             const int64_t p1 = (p0 + H < pe) ? p0 + H : pe;
             for (int64_t p = p0 + lane; p < p1; p += 256) {
                 int32_t j[4];
@@ -233,62 +319,77 @@ __device__ __forceinline__ long long gb_push_phase(int64_t nwords_u, const uint6
                 }
                 added += gb_push_targets(j, ok, mbits, mcomp, tbits);
             }
-            continue;
         }
-        const int64_t w = unit - nhubs;
-        const uint64_t word = ubits[w];
-        if (!word) continue;
-        int64_t p0 = 0;
-        int len = 0;
-        if ((word >> lane) & 1ULL) {
-            const int64_t k = (w << 6) + lane;
-            p0 = prow[k];
-            const int64_t d = prow[k + 1] - p0;
-            len = d > H ? 0 : (int)d;  // hubs: done by their chunks
+    }
+    // frontier words, 4 per wave step (lanes 0-3 load them)
+    for (int64_t w0 = wave * 4; w0 < nwords_u; w0 += nwaves * 4) {
+        const int64_t wl = w0 + (lane & 3);
+        const uint64_t mine = wl < nwords_u ? ubits[wl] : 0;
+        if (!__ballot(mine != 0)) continue;
+        int64_t p0[4], d[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint64_t word = __shfl(mine, u, 64);
+            p0[u] = d[u] = 0;
+            if ((word >> lane) & 1ULL) {
+                const int64_t k = ((w0 + u) << 6) + lane;
+                p0[u] = prow[k];
+                d[u] = prow[k + 1] - p0[u];
+            }
         }
-        int incl = len;
-        for (int off = 1; off < 64; off <<= 1) {
-            const int y = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += y;
+        int n = 0;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const bool in = d[u] > 0 && d[u] <= H;  // hubs: done by their chunks
+            const unsigned long long bb = __ballot(in);
+            if (in) {
+                const int i = n + __popcll(bb & lt);
+                L.p[i] = p0[u];
+                L.rem[i] = (int32_t)d[u];
+            }
+            n += __popcll(bb);
         }
-        const int excl = incl - len;
-        const int total = __shfl(incl, 63, 64);
+        if (!n) continue;
+        gb_wave_sync();
+        const int total = gb_wlist_round(L, n, 1 << 30, lane);
         for (int e0 = 0; e0 < total; e0 += 256) {
             int32_t j[4];
             bool ok[4];
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const int e = e0 + lane + 64 * u;
-                int lo = 0;  // owner row: first lane whose inclusive prefix exceeds e
-#pragma unroll
-                for (int st = 32; st > 0; st >>= 1)
-                    if (__shfl(incl, lo + st - 1, 64) <= e) lo += st;
-                const int64_t ps = __shfl(p0, lo, 64);
-                const int ex = __shfl(excl, lo, 64);
                 ok[u] = e < total;
-                j[u] = ok[u] ? pcol[ps + (e - ex)] : 0;
+                j[u] = 0;
+                if (ok[u]) {
+                    const int s = gb_wlist_find(L, n, e);
+                    j[u] = pcol[L.p[s] + (e - gb_wlist_start(L, s))];
+                }
             }
             added += gb_push_targets(j, ok, mbits, mcomp, tbits);
         }
+        gb_wave_sync();
     }
     return added;
 }
 
 // Pull (bottom-up) for iso results: only presence is computed.  A wave takes
 // PULL_U 64-row bitmap words at a time, one lane per row of each: a lane walks
-// its own rows two edges a step (neighbouring rows are neighbouring in colidx,
-// so the loads coalesce), stopping at the first k present in u; rows still
-// open after 8 edges are finished eight at a time, eight lanes per row.
+// its own rows four edges a step (neighbouring rows are neighbouring in colidx,
+// so the loads coalesce), stopping at the first k present in u.  Rows still
+// open after 8 edges go into the wave's segment list and are walked as one
+// edge stream in rounds (at most `cap` edges per row per round, cap doubling),
+// dropping the rows that found a k after each round.
 __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int64_t *__restrict__ rowptr,
                                                       const int32_t *__restrict__ colidx,
                                                       const uint64_t *__restrict__ ubits,
                                                       const uint64_t *__restrict__ mbits, bool mcomp,
-                                                      uint64_t *__restrict__ tbits) {
+                                                      uint64_t *__restrict__ tbits, gb_wlist &L) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const int64_t nwords = (nrows + 63) >> 6;
     const uint64_t tail = (nrows & 63) ? ((1ULL << (nrows & 63)) - 1) : ~0ULL;
+    const unsigned long long lt = (1ULL << lane) - 1;
     long long cnt = 0;
     for (int64_t w0 = wave * PULL_U; w0 < nwords; w0 += nwaves * PULL_U) {
         const int64_t wl = w0 + (lane & (PULL_U - 1));
@@ -309,7 +410,7 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
                 p1[u] = rowptr[r + 1];
             }
         }
-        for (int it = 0; it < 4; it++) {
+        for (int it = 0; it < 2; it++) {
             bool go[PULL_U], any = false;
 #pragma unroll
             for (int u = 0; u < PULL_U; u++) {
@@ -317,56 +418,114 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
                 any = any || go[u];
             }
             if (!__ballot(any)) break;
-            int k0[PULL_U], k1[PULL_U];
+            int k[PULL_U][4];
 #pragma unroll
             for (int u = 0; u < PULL_U; u++) {
+#pragma unroll
+                for (int t = 0; t < 4; t++) k[u][t] = -1;
                 if (go[u]) {
-                    k0[u] = colidx[p[u]];
-                    k1[u] = (p[u] + 1 < p1[u]) ? colidx[p[u] + 1] : k0[u];
+#pragma unroll
+                    for (int t = 0; t < 4; t++)
+                        if (p[u] + t < p1[u]) k[u][t] = colidx[p[u] + t];
                 }
             }
 #pragma unroll
             for (int u = 0; u < PULL_U; u++) {
                 if (go[u]) {
-                    found[u] = (gb_bit(ubits, k0[u]) + gb_bit(ubits, k1[u])) != 0;
-                    p[u] += 2;
+                    int f = 0;
+#pragma unroll
+                    for (int t = 0; t < 4; t++) f += k[u][t] >= 0 && gb_bit(ubits, k[u][t]);
+                    found[u] = f != 0;
+                    p[u] += 4;
                 }
             }
         }
+        // rows still open -> segment list
+        int n = 0;
 #pragma unroll
         for (int u = 0; u < PULL_U; u++) {
-            // rows still open: eight at a time, eight lanes per row
-            unsigned long long pend = __ballot(live[u] && !found[u] && p[u] < p1[u]);
-            unsigned long long hit = 0;
-            const int g = lane >> 3, gl = lane & 7;
-            while (pend) {
-                const unsigned long long round = pend;
-                unsigned long long t = pend;
-                int mine = -1;
-                for (int i = 0; i < 8 && t; i++) {
-                    const int b = __ffsll(t) - 1;
-                    t &= t - 1;
-                    if (i == g) mine = b;
-                }
-                pend = t;
-                const int src = mine < 0 ? 0 : mine;
-                const int64_t q0 = __shfl(p[u], src, 64), q1 = __shfl(p1[u], src, 64);
-                bool f = false;
-                if (mine >= 0) {
-                    for (int64_t q = q0 + gl; q < q1; q += 8) {
-                        f = gb_bit(ubits, colidx[q]);
-                        if ((__ballot(f) >> (g * 8)) & 0xFFULL) break;
+            const bool pd = live[u] && !found[u] && p[u] < p1[u];
+            const unsigned long long bb = __ballot(pd);
+            if (pd) {
+                const int i = n + __popcll(bb & lt);
+                L.p[i] = p[u];
+                L.rem[i] = (int32_t)(p1[u] - p[u]);
+                L.id[i] = (int16_t)(u * 64 + lane);
+            }
+            n += __popcll(bb);
+        }
+        unsigned long long hitw[PULL_U];
+#pragma unroll
+        for (int u = 0; u < PULL_U; u++) hitw[u] = 0;
+        int cap = 16;
+        while (n) {
+            gb_wave_sync();
+            const int total = gb_wlist_round(L, n, cap, lane);
+            for (int e0 = 0; e0 < total; e0 += 256) {
+                int k[4], s[4];
+                bool ok[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int e = e0 + lane + 64 * u;
+                    ok[u] = e < total;
+                    s[u] = 0;
+                    k[u] = 0;
+                    if (ok[u]) {
+                        s[u] = gb_wlist_find(L, n, e);
+                        k[u] = colidx[L.p[s[u]] + (e - gb_wlist_start(L, s[u]))];
                     }
                 }
-                const unsigned long long fb = __ballot(f);
-                t = round;
-                for (int i = 0; i < 8 && t; i++) {
-                    const int b = __ffsll(t) - 1;
-                    t &= t - 1;
-                    if ((fb >> (i * 8)) & 0xFFULL) hit |= 1ULL << b;
-                }
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    if (ok[u] && gb_bit(ubits, k[u])) L.hit[s[u]] = 1;
             }
-            if ((hit >> lane) & 1ULL) found[u] = true;
+            gb_wave_sync();
+            // survivors of the round, compacted in place (chunks of 64, in order)
+            int m = 0;
+            for (int c0 = 0; c0 < n; c0 += 64) {
+                const int i = c0 + lane;
+                bool alive = false, hit = false;
+                int64_t np = 0;
+                int32_t nr = 0;
+                int16_t id = 0;
+                if (i < n) {
+                    const int32_t taken = L.pref[i] - gb_wlist_start(L, i);
+                    hit = L.hit[i] != 0;
+                    id = L.id[i];
+                    np = L.p[i] + taken;
+                    nr = L.rem[i] - taken;
+                    alive = !hit && nr > 0;
+                }
+#pragma unroll
+                for (int u = 0; u < PULL_U; u++) {
+                    const unsigned long long hb = __ballot(hit && (id >> 6) == u);
+                    // lane `id & 63` of word u found a k: collect the bits by row lane
+                    unsigned long long bits = 0;
+                    unsigned long long t = hb;
+                    while (t) {
+                        const int l = __ffsll(t) - 1;
+                        t &= t - 1;
+                        bits |= 1ULL << (__shfl((int)id, l, 64) & 63);
+                    }
+                    hitw[u] |= bits;
+                }
+                const unsigned long long ab = __ballot(alive);
+                gb_wave_sync();
+                if (alive) {
+                    const int j = m + __popcll(ab & lt);
+                    L.p[j] = np;
+                    L.rem[j] = nr;
+                    L.id[j] = id;
+                }
+                m += __popcll(ab);
+                gb_wave_sync();
+            }
+            n = m;
+            cap = cap < (1 << 20) ? cap * 2 : cap;
+        }
+#pragma unroll
+        for (int u = 0; u < PULL_U; u++) {
+            if ((hitw[u] >> lane) & 1ULL) found[u] = true;
             const unsigned long long word = __ballot(found[u]);
             if (lane == 0 && w0 + u < nwords) {
                 tbits[w0 + u] = word;
@@ -385,14 +544,24 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
     const int32_t *__restrict__ pcol, const int32_t *__restrict__ hubs, int64_t nhubs, int64_t H,
     const uint64_t *__restrict__ mbits, bool mcomp, uint64_t *__restrict__ tbits,
     unsigned long long *__restrict__ tcount, unsigned long long *__restrict__ gst,
-    const unsigned long long *__restrict__ dst) {
+    const unsigned long long *__restrict__ dst, gb_host_slot *pub, long long pub_seq) {
+    __shared__ gb_wlist lists[WAVES_PER_BLOCK];
+    gb_wlist &L = lists[threadIdx.x >> 6];
     long long cnt;
     if (dst && dst[ST_PUSH])
         cnt = gb_push_phase(nwords_u, ubits, prow, pcol, hubs, nhubs, H, mbits, mcomp,
-                            (unsigned long long *)tbits);
+                            (unsigned long long *)tbits, L);
     else
-        cnt = gb_pull_iso_phase(nrows, rowptr, colidx, ubits, mbits, mcomp, tbits);
-    gb_grid_add(cnt, tcount, gst);
+        cnt = gb_pull_iso_phase(nrows, rowptr, colidx, ubits, mbits, mcomp, tbits, L);
+    long long tot;
+    if (gb_grid_sum(cnt, gst, &tot)) {
+        const unsigned long long nv = atomicAdd(tcount, (unsigned long long)tot) + (unsigned long long)tot;
+        if (pub) {  // hand the count to the host without a copy (gb_host_slot_wait)
+            __hip_atomic_store(&pub->value, (long long)nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __threadfence_system();
+            __hip_atomic_store(&pub->seq, pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 // hub-chunk table of a CSR: pieces per row, then (row, piece) pairs
@@ -502,10 +671,10 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             if (can_push) {
                 // prep (frontier edges -> direction, zeroed output, iso value), then one work launch
                 lk.lock();
-                units = std::max<int64_t>(units, Apush->nhubs + uw);
+                units = std::max<int64_t>(units, std::max<int64_t>((Apush->nhubs + 15) / 16, (uw + 3) / 4));
                 gb_dir_rule rule{mask.count, mask.comp, n, A.nvals, alpha, dir_knob == 2};
                 const unsigned prep_grid =
-                    (unsigned)std::max<int64_t>(1, std::min<int64_t>((uw + 4 * PULL_U - 1) / (4 * PULL_U), 1024));
+                    (unsigned)std::max<int64_t>(1, std::min<int64_t>((uw + 63) / 64, 1024));
                 if (flip)
                     hipLaunchKernelGGL((k_dir_prep<SRT, X, Z, true>), dim3(prep_grid), dim3(SPMV_BLOCK), 0,
                                        gb_stream(), srf, u.bits, uw, Apush->rowptr, gst, dst, T.bits, nw,
@@ -532,8 +701,10 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
                                u.bits, can_push ? Apush->rowptr : nullptr, can_push ? Apush->colidx : nullptr,
                                can_push ? Apush->hubs : nullptr, can_push ? Apush->nhubs : 0,
                                can_push ? Apush->hub_H : 1, mask.bits, mask.comp, T.bits,
-                               (unsigned long long *)T.d_nvals, gst, can_push ? dst : nullptr);
+                               (unsigned long long *)T.d_nvals, gst, can_push ? dst : nullptr,
+                               T.pub ? gb_host_slot_device(T.pub) : nullptr, (long long)T.pub_seq);
             GB_LAUNCH_CHECK();
+            T.published = T.pub != nullptr;
             return;
         }
         gb_memset(T.d_nvals, 0, sizeof(int64_t));

@@ -136,7 +136,12 @@ void gb_obj_free_storage(GB_Obj *A) {
 int64_t gb_nvals(GB_Obj *A) {
     if (A->kind == GB_KIND_MATRIX) return A->nvals;
     if (!A->nvals_valid) {
-        A->nvals = gb_read_i64(A->d_nvals);
+        int64_t v;
+        if (A->pub && A->pub_seq && A->pub_epoch == gb_epoch() && gb_host_slot_wait(A->pub, A->pub_seq, &v)) {
+            A->nvals = v;  // published by the kernel that produced d_nvals
+        } else {
+            A->nvals = gb_read_i64(A->d_nvals);
+        }
         A->nvals_valid = true;
     }
     return A->nvals;
@@ -197,6 +202,7 @@ void gb_install_bitmap(GB_Obj *C, int64_t n, uint64_t *bits, void *dense, bool i
             gb_bitmap_count(bits, n, C->d_nvals);
         }
         C->nvals_valid = false;
+        C->pub_seq = 0;
         return;
     }
     // matrix target (n x 1): bitmap -> CSR
@@ -1091,6 +1097,8 @@ GrB_Info GrB_Matrix_free(GrB_Matrix *A) {
     GrB_Info info = gb_api(nullptr, [&] {
         gb_obj_free_storage(o);
         gb_free(o->d_nvals);
+        gb_host_slot_release(o->pub);
+        o->pub = nullptr;
     });
     o->magic = GB_FREED;
     delete o;

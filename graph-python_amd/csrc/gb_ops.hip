@@ -65,8 +65,18 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
         push = &pv;
     }
     gb_vec_result T;
+    if (w->kind != GB_KIND_MATRIX) {
+        if (!w->pub) w->pub = gb_host_slot_alloc();
+        T.pub = w->pub;
+        T.pub_seq = gb_next_pub_seq();
+    }
     gb_spmv(T, av, push, uv, m, sr, vxm);
-    gb_writeback_vector(w, T, mask, d, accum, true);
+    const bool direct = gb_writeback_vector(w, T, mask, d, accum, true);
+    if (direct && T.published) {
+        // w's count is the one the kernel published; valid until more work is enqueued
+        w->pub_seq = T.pub_seq;
+        w->pub_epoch = gb_epoch();
+    }
 }
 
 // ================================================================== mxm
@@ -446,8 +456,10 @@ __global__ __launch_bounds__(OPS_BLOCK) void k_assign_all_scalar(
     gb_grid_add(delta, count, gst);
 }
 
-// w<M>(:) = x, M a plain (non-complemented) mask, no replace: a thread per
-// 64-bit word; only words with selected bits are touched.
+// w<M>(:) = x, M a plain (non-complemented) mask, no replace: a wave takes 64
+// mask words per step, one per lane (each lane updates its presence word);
+// then the selected values of each non-zero word are written by the whole
+// wave, one lane per position (coalesced stores).
 template <class T>
 __global__ __launch_bounds__(OPS_BLOCK) void k_assign_mask_words(int64_t nwords, uint64_t *__restrict__ cbits,
                                                                  T *__restrict__ cvals,
@@ -456,19 +468,25 @@ __global__ __launch_bounds__(OPS_BLOCK) void k_assign_mask_words(int64_t nwords,
                                                                  unsigned long long *__restrict__ count,
                                                                  unsigned long long *__restrict__ gst) {
     const bool iso_true = miso ? gb_dyn_nonzero(miso, miso_code) : true;
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     long long delta = 0;
     if (iso_true) {
-        for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nwords;
-             w += (int64_t)gridDim.x * blockDim.x) {
-            uint64_t m = mbits[w];
-            if (!m) continue;
-            const uint64_t c = cbits[w], nwd = c | m;
-            if (nwd != c) cbits[w] = nwd;
-            delta += (long long)__popcll(nwd) - (long long)__popcll(c);
-            while (m) {
-                const int b = __ffsll((unsigned long long)m) - 1;
-                m &= m - 1;
-                cvals[(w << 6) + b] = x;
+        for (int64_t base = wave * 64; base < nwords; base += nwaves * 64) {
+            const int64_t w = base + lane;
+            const uint64_t m = w < nwords ? mbits[w] : 0;
+            if (m) {
+                const uint64_t c = cbits[w], nwd = c | m;
+                if (nwd != c) cbits[w] = nwd;
+                delta += (long long)__popcll(nwd) - (long long)__popcll(c);
+            }
+            unsigned long long nz = __ballot(m != 0);
+            while (nz) {
+                const int l = __ffsll(nz) - 1;
+                nz &= nz - 1;
+                const uint64_t mw = __shfl(m, l, 64);
+                if ((mw >> lane) & 1ULL) cvals[((base + l) << 6) + lane] = x;
             }
         }
     }
@@ -519,7 +537,7 @@ static bool assign_all_scalar_fast(GB_Obj *w, GB_Obj *mask, const char *xc, cons
         memcpy(&xv, xc, sizeof(T));
         if (n && m.bits && !m.comp && !d.replace)
             hipLaunchKernelGGL(k_assign_mask_words<T>,
-                               dim3((unsigned)std::min<int64_t>((gb_words(n) + OPS_BLOCK - 1) / OPS_BLOCK, 1024)),
+                               dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((gb_words(n) + 255) / 256, 1024))),
                                dim3(OPS_BLOCK), 0, gb_stream(), gb_words(n), w->bits, (T *)w->dense, m.bits, m.iso_val,
                                m.iso_code, xv, (unsigned long long *)w->d_nvals, gb_device_state());
         else if (n)

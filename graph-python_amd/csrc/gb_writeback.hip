@@ -210,7 +210,7 @@ static void free_vec_result(gb_vec_result &T) {
     T.d_nvals = nullptr;
 }
 
-void gb_writeback_vector(GB_Obj *C, gb_vec_result &T, GB_Obj *M, const gb_desc &d, GrB_BinaryOp accum,
+bool gb_writeback_vector(GB_Obj *C, gb_vec_result &T, GB_Obj *M, const gb_desc &d, GrB_BinaryOp accum,
                          bool t_within_mask) {
     const int ct = C->type->code;
     const int64_t n = T.n;
@@ -222,7 +222,7 @@ void gb_writeback_vector(GB_Obj *C, gb_vec_result &T, GB_Obj *M, const gb_desc &
         T.bits = nullptr;
         T.dense = nullptr;
         T.d_nvals = nullptr;
-        return;
+        return true;
     }
     // general merge
     int wcode = ct;
@@ -264,6 +264,7 @@ void gb_writeback_vector(GB_Obj *C, gb_vec_result &T, GB_Obj *M, const gb_desc &
         ovals = o2;
     }
     gb_install_bitmap(C, n, obits, ovals, false, cnt);
+    return false;
 }
 
 // ================================================================== matrices

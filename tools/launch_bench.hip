@@ -12,7 +12,20 @@ static double now_us() {
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-int main() {
+__global__ void k_publish(volatile long long *host, long long seq) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        __threadfence_system();
+        host[0] = seq;
+    }
+}
+
+int main(int argc, char **argv) {
+    if (argc > 1 && argv[1][0] == 's') {
+        printf("hipSetDeviceFlags(spin) -> %d\n", (int)hipSetDeviceFlags(hipDeviceScheduleSpin));
+    }
+    if (argc > 1 && argv[1][0] == 'y') {
+        printf("hipSetDeviceFlags(yield) -> %d\n", (int)hipSetDeviceFlags(hipDeviceScheduleYield));
+    }
     hipStream_t s;
     hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
     int *d;
@@ -84,5 +97,38 @@ int main() {
     }
     t1 = now_us();
     printf("1 launch + sync: %.2f us\n", (t1 - t0) / 200);
+    // kernel publishes a sequence number into pinned host memory; host spins on it
+    volatile long long *mb;
+    hipHostMalloc((void **)&mb, 64, hipHostMallocCoherent | hipHostMallocMapped);
+    mb[0] = 0;
+    t0 = now_us();
+    for (int i = 1; i <= 500; i++) {
+        hipLaunchKernelGGL(k_empty, dim3(1024), dim3(256), 0, s, d);
+        hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, s, mb, (long long)i);
+        while (mb[0] != i) {
+        }
+    }
+    t1 = now_us();
+    printf("launch+publish+spin round trip: %.2f us\n", (t1 - t0) / 500);
+    t0 = now_us();
+    for (int i = 501; i <= 1000; i++) {
+        hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, s, mb, (long long)i);
+        while (mb[0] != i) {
+        }
+    }
+    t1 = now_us();
+    printf("publish-only+spin round trip: %.2f us\n", (t1 - t0) / 500);
+    hipStreamSynchronize(s);
+    // event-based wait
+    hipEvent_t ev;
+    hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    t0 = now_us();
+    for (int i = 0; i < 200; i++) {
+        hipLaunchKernelGGL(k_empty, dim3(1024), dim3(256), 0, s, d);
+        hipEventRecord(ev, s);
+        hipEventSynchronize(ev);
+    }
+    t1 = now_us();
+    printf("launch+event sync: %.2f us\n", (t1 - t0) / 200);
     return 0;
 }
