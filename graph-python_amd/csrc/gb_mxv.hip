@@ -399,16 +399,20 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
         if (wl >= nwords) mine = 0;
         bool live[PULL_U], found[PULL_U];
         int64_t p[PULL_U], p1[PULL_U];
+        // row bounds are loaded for every row, independently of the mask word
+#pragma unroll
+        for (int u = 0; u < PULL_U; u++) {
+            const int64_t r = ((w0 + u) << 6) + lane;
+            p[u] = p1[u] = 0;
+            if (r < nrows) {
+                p[u] = rowptr[r];
+                p1[u] = rowptr[r + 1];
+            }
+        }
 #pragma unroll
         for (int u = 0; u < PULL_U; u++) {
             live[u] = (__shfl(mine, u, 64) >> lane) & 1ULL;
             found[u] = false;
-            p[u] = p1[u] = 0;
-            if (live[u]) {
-                const int64_t r = ((w0 + u) << 6) + lane;
-                p[u] = rowptr[r];
-                p1[u] = rowptr[r + 1];
-            }
         }
         for (int it = 0; it < 2; it++) {
             bool go[PULL_U], any = false;
@@ -619,7 +623,20 @@ static bool idempotent_monoid(int m) {
            m == GBAMD_MON_LAND || m == GBAMD_MON_BOR || m == GBAMD_MON_BAND;
 }
 
-static std::mutex g_dir_mu;  // keeps the prep/push/pull launches of one call adjacent
+static std::mutex g_dir_mu;
+
+// blocks of k_iso_work the device holds at once (the work grid is sized to one wave of blocks)
+static int64_t iso_work_resident_blocks() {
+    static int64_t cap = 0;
+    if (!cap) {
+        int dev = 0, cus = 0, per = 0;
+        GB_HIP(hipGetDevice(&dev));
+        GB_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        GB_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_iso_work, SPMV_BLOCK, 0));
+        cap = std::max<int64_t>(1, (int64_t)cus * std::max(per, 1));
+    }
+    return cap;
+}  // keeps the prep/push/pull launches of one call adjacent
 
 bool gb_spmv_result_iso(GrB_Semiring sr, bool a_iso, bool u_iso, bool flip) {
     gb_sr_info info = gb_sr_describe(sr);
@@ -673,8 +690,10 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
                 lk.lock();
                 units = std::max<int64_t>(units, std::max<int64_t>((Apush->nhubs + 15) / 16, (uw + 3) / 4));
                 gb_dir_rule rule{mask.count, mask.comp, n, A.nvals, alpha, dir_knob == 2};
+                int64_t pcap = gb_knob("prep_grid");
+                if (pcap <= 0) pcap = 1024;
                 const unsigned prep_grid =
-                    (unsigned)std::max<int64_t>(1, std::min<int64_t>((uw + 63) / 64, 1024));
+                    (unsigned)std::max<int64_t>(1, std::min<int64_t>((uw + 63) / 64, pcap));
                 if (flip)
                     hipLaunchKernelGGL((k_dir_prep<SRT, X, Z, true>), dim3(prep_grid), dim3(SPMV_BLOCK), 0,
                                        gb_stream(), srf, u.bits, uw, Apush->rowptr, gst, dst, T.bits, nw,
@@ -696,7 +715,9 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
                                        (const X *)av, (const X *)uv, (Z *)T.dense);
                 GB_LAUNCH_CHECK();
             }
-            const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 3) / 4, 4096));
+            int64_t gcap = gb_knob("iso_work_grid");
+            if (gcap <= 0) gcap = iso_work_resident_blocks();
+            const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 3) / 4, gcap));
             hipLaunchKernelGGL(k_iso_work, dim3(grid), dim3(SPMV_BLOCK), 0, gb_stream(), n, A.rowptr, A.colidx, uw,
                                u.bits, can_push ? Apush->rowptr : nullptr, can_push ? Apush->colidx : nullptr,
                                can_push ? Apush->hubs : nullptr, can_push ? Apush->nhubs : 0,
