@@ -91,6 +91,11 @@ struct GB_Matrix_opaque {
     // (valid while pub_epoch == gb_epoch(): nothing enqueued since)
     struct gb_host_slot *pub;
     uint64_t pub_seq, pub_epoch;
+    // d_nvals[1] holds the edge count of this vector's entries in the rows of the
+    // push-orientation CSR whose rowptr is hint_key (written by the BFS SpMV that
+    // produced it; a stale hint only affects the push/pull choice, never results)
+    bool hint_valid;
+    const void *hint_key;
     std::string err;
 };
 typedef GB_Matrix_opaque GB_Obj;
@@ -225,6 +230,8 @@ struct gb_bitmap_view {
     const void *vals = nullptr;
     bool iso = false;
     int tcode = 0;
+    const long long *mf_hint = nullptr;  // device edge count of the entries (see GB_Obj::hint_key)
+    const void *hint_key = nullptr;
     gb_scratch own;
 };
 void gb_get_bitmap(gb_bitmap_view &v, GB_Obj *A);
@@ -297,6 +304,7 @@ struct gb_vec_result {  // bitmap, type code ztype
     gb_host_slot *pub = nullptr;  // if set, the producing kernel publishes nvals here
     uint64_t pub_seq = 0;
     bool published = false;       // set by the producer when it did publish
+    const void *hint_key = nullptr;  // set when d_nvals[1] holds the edge-count hint
 };
 struct gb_mat_result {  // CSR
     int64_t nrows = 0, ncols = 0, nvals = 0;

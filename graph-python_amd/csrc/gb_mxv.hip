@@ -125,6 +125,18 @@ struct gb_dir_rule {
     int force_push;
 };
 
+// Beamer's rule: push while the frontier's edges m_f (times alpha) are fewer
+// than the edges the pull would examine, estimated as open rows x average degree
+__device__ __forceinline__ bool gb_dir_decide(long long mf, const gb_dir_rule &rule) {
+    int64_t open = rule.n_out;  // rows the pull kernel would visit
+    if (rule.mask_count) {
+        const int64_t mc = *rule.mask_count;
+        open = rule.mcomp ? (rule.n_out - mc) : mc;
+    }
+    const double avg = rule.n_out ? (double)rule.nnz / (double)rule.n_out : 0.0;
+    return rule.force_push || ((double)mf * (double)rule.alpha < (double)open * avg);
+}
+
 // Prep: m_f = edges of the frontier in the push orientation (one lane per
 // frontier bit); zeroes the output bitmap and count; writes the iso result
 // value.  The block that completes the grid-wide sum of m_f applies
@@ -174,23 +186,15 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_dir_prep(
         }
     }
     long long total;
-    if (gb_grid_sum(mf, gst, &total)) {
-        int64_t open = rule.n_out;  // rows the pull kernel would visit
-        if (rule.mask_count) {
-            const int64_t mc = *rule.mask_count;
-            open = rule.mcomp ? (rule.n_out - mc) : mc;
-        }
-        const double avg = rule.n_out ? (double)rule.nnz / (double)rule.n_out : 0.0;
-        const bool push = rule.force_push || ((double)total * (double)rule.alpha < (double)open * avg);
-        dst[ST_PUSH] = push ? 1ULL : 0ULL;
-    }
+    if (gb_grid_sum(mf, gst, &total)) dst[ST_PUSH] = gb_dir_decide(total, rule) ? 1ULL : 0ULL;
 }
 
 // set the output bits of up to 4 targets per lane (unmasked, not yet set);
 // returns how many bits this lane turned on
 __device__ __forceinline__ long long gb_push_targets(const int32_t (&j)[4], bool (&ok)[4],
                                                      const uint64_t *__restrict__ mbits, bool mcomp,
-                                                     unsigned long long *__restrict__ tbits) {
+                                                     unsigned long long *__restrict__ tbits,
+                                                     const int64_t *__restrict__ hprow, long long &mfn) {
     if (mbits) {
 #pragma unroll
         for (int u = 0; u < 4; u++)
@@ -205,7 +209,10 @@ __device__ __forceinline__ long long gb_push_targets(const int32_t (&j)[4], bool
         const unsigned long long m = 1ULL << (j[u] & 63);
         if (ok[u] && !(cur[u] & m)) {
             const unsigned long long old = atomicOr(&tbits[j[u] >> 6], m);
-            if (!(old & m)) added++;
+            if (!(old & m)) {
+                added++;
+                if (hprow) mfn += hprow[j[u] + 1] - hprow[j[u]];  // edges of the next frontier
+            }
         }
     }
     return added;
@@ -284,7 +291,8 @@ __device__ __forceinline__ long long gb_push_phase(int64_t nwords_u, const uint6
                                                   const int64_t *__restrict__ prow, const int32_t *__restrict__ pcol,
                                                   const int32_t *__restrict__ hubs, int64_t nhubs, int64_t H,
                                                   const uint64_t *__restrict__ mbits, bool mcomp,
-                                                  unsigned long long *__restrict__ tbits, gb_wlist &L) {
+                                                  unsigned long long *__restrict__ tbits, gb_wlist &L,
+                                                  const int64_t *__restrict__ hprow, long long &mfn) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -317,7 +325,7 @@ __device__ __forceinline__ long long gb_push_phase(int64_t nwords_u, const uint6
                     ok[u] = p + 64 * u < p1;
                     j[u] = ok[u] ? pcol[p + 64 * u] : 0;
                 }
-                added += gb_push_targets(j, ok, mbits, mcomp, tbits);
+                added += gb_push_targets(j, ok, mbits, mcomp, tbits, hprow, mfn);
             }
         }
     }
@@ -365,7 +373,7 @@ __device__ __forceinline__ long long gb_push_phase(int64_t nwords_u, const uint6
                     j[u] = pcol[L.p[s] + (e - gb_wlist_start(L, s))];
                 }
             }
-            added += gb_push_targets(j, ok, mbits, mcomp, tbits);
+            added += gb_push_targets(j, ok, mbits, mcomp, tbits, hprow, mfn);
         }
         gb_wave_sync();
     }
@@ -383,7 +391,8 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
                                                       const int32_t *__restrict__ colidx,
                                                       const uint64_t *__restrict__ ubits,
                                                       const uint64_t *__restrict__ mbits, bool mcomp,
-                                                      uint64_t *__restrict__ tbits, gb_wlist &L) {
+                                                      uint64_t *__restrict__ tbits, gb_wlist &L,
+                                                      const int64_t *__restrict__ hprow, long long &mfn) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -409,10 +418,12 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
                 p1[u] = rowptr[r + 1];
             }
         }
+        int32_t dg[PULL_U];
 #pragma unroll
         for (int u = 0; u < PULL_U; u++) {
             live[u] = (__shfl(mine, u, 64) >> lane) & 1ULL;
             found[u] = false;
+            dg[u] = (int32_t)(p1[u] - p[u]);
         }
         for (int it = 0; it < 2; it++) {
             bool go[PULL_U], any = false;
@@ -536,35 +547,104 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
                 cnt += __popcll(word);
             }
         }
+        if (hprow) {
+            // edges of the next frontier, estimated by the rows' pull-orientation
+            // length (already loaded; exact for symmetric matrices): a hint for the
+            // next call's push/pull choice only
+#pragma unroll
+            for (int u = 0; u < PULL_U; u++)
+                if (found[u]) mfn += dg[u];
+        }
     }
     return cnt;
 }
 
-// One launch does the chosen direction (dst[ST_PUSH], set by k_dir_prep; dst
-// null: pull only).  Counts the output bits into *tcount.
+// z = mult(a0, u0) for an iso result, types known only at run time (z is x's
+// type or bool: the builtin semirings' z types)
+template <class X>
+__device__ void gb_iso_eval_x(int mul, bool zbool, bool flip, const void *a0, const void *u0, void *out) {
+    const X a = a0 ? *(const X *)a0 : X(), b = u0 ? *(const X *)u0 : X();
+    const X x = flip ? b : a, y = flip ? a : b;
+    if (zbool) *(bool *)out = gb_binop_z<X, bool>(mul, x, y, 0, 0, 0);
+    else *(X *)out = gb_binop_z<X, X>(mul, x, y, 0, 0, 0);
+}
+__device__ void gb_iso_eval(int mul, int xcode, int zcode, bool flip, const void *a0, const void *u0, void *out) {
+    const bool zb = zcode == GBAMD_T_BOOL && xcode != GBAMD_T_BOOL;
+    switch (xcode) {
+    case GBAMD_T_BOOL: gb_iso_eval_x<bool>(mul, zb, flip, a0, u0, out); break;
+    case GBAMD_T_INT8: gb_iso_eval_x<int8_t>(mul, zb, flip, a0, u0, out); break;
+    case GBAMD_T_UINT8: gb_iso_eval_x<uint8_t>(mul, zb, flip, a0, u0, out); break;
+    case GBAMD_T_INT16: gb_iso_eval_x<int16_t>(mul, zb, flip, a0, u0, out); break;
+    case GBAMD_T_UINT16: gb_iso_eval_x<uint16_t>(mul, zb, flip, a0, u0, out); break;
+    case GBAMD_T_INT32: gb_iso_eval_x<int32_t>(mul, zb, flip, a0, u0, out); break;
+    case GBAMD_T_UINT32: gb_iso_eval_x<uint32_t>(mul, zb, flip, a0, u0, out); break;
+    case GBAMD_T_INT64: gb_iso_eval_x<int64_t>(mul, zb, flip, a0, u0, out); break;
+    case GBAMD_T_UINT64: gb_iso_eval_x<uint64_t>(mul, zb, flip, a0, u0, out); break;
+    case GBAMD_T_FP32: gb_iso_eval_x<float>(mul, zb, flip, a0, u0, out); break;
+    case GBAMD_T_FP64: gb_iso_eval_x<double>(mul, zb, flip, a0, u0, out); break;
+    default: break;
+    }
+}
+
+struct gb_iso_args {
+    // direction: from the frontier's edge-count hint (the vector's producer
+    // computed it), else from k_dir_prep's decision, else pull
+    const long long *mf_hint;
+    gb_dir_rule rule;
+    const unsigned long long *dst;
+    // next-frontier hint: edges of the output's entries in rows of hprow
+    const int64_t *hprow;
+    long long *mf_out;
+    // iso value of the result (nullptr: written elsewhere)
+    int mul, xcode, zcode;
+    bool flip;
+    const void *a0, *u0;
+    void *iso_out;
+    // host mailbox for the count
+    gb_host_slot *pub;
+    long long pub_seq;
+    // a bitmap to zero for the next call's push output
+    uint64_t *spare;
+    int64_t spare_words;
+};
+
+// One launch does the chosen direction and finishes the result: count
+// (stored, no prior zeroing needed), next-frontier hint, iso value, mailbox.
 __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
     int64_t nrows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ colidx,
     int64_t nwords_u, const uint64_t *__restrict__ ubits, const int64_t *__restrict__ prow,
     const int32_t *__restrict__ pcol, const int32_t *__restrict__ hubs, int64_t nhubs, int64_t H,
     const uint64_t *__restrict__ mbits, bool mcomp, uint64_t *__restrict__ tbits,
-    unsigned long long *__restrict__ tcount, unsigned long long *__restrict__ gst,
-    const unsigned long long *__restrict__ dst, gb_host_slot *pub, long long pub_seq) {
+    unsigned long long *__restrict__ tcount, unsigned long long *__restrict__ gst, gb_iso_args a) {
     __shared__ gb_wlist lists[WAVES_PER_BLOCK];
     gb_wlist &L = lists[threadIdx.x >> 6];
-    long long cnt;
-    if (dst && dst[ST_PUSH])
+    bool push = false;
+    if (a.mf_hint) push = gb_dir_decide(*a.mf_hint, a.rule);
+    else if (a.dst) push = a.dst[ST_PUSH] != 0;
+    if (a.spare) {
+        for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < a.spare_words;
+             w += (int64_t)gridDim.x * blockDim.x)
+            a.spare[w] = 0;
+    }
+    long long mfn = 0, cnt;
+    if (push)
         cnt = gb_push_phase(nwords_u, ubits, prow, pcol, hubs, nhubs, H, mbits, mcomp,
-                            (unsigned long long *)tbits, L);
+                            (unsigned long long *)tbits, L, a.hprow, mfn);
     else
-        cnt = gb_pull_iso_phase(nrows, rowptr, colidx, ubits, mbits, mcomp, tbits, L);
+        cnt = gb_pull_iso_phase(nrows, rowptr, colidx, ubits, mbits, mcomp, tbits, L, a.hprow, mfn);
     long long tot;
     if (gb_grid_sum(cnt, gst, &tot)) {
-        const unsigned long long nv = atomicAdd(tcount, (unsigned long long)tot) + (unsigned long long)tot;
-        if (pub) {  // hand the count to the host without a copy (gb_host_slot_wait)
-            __hip_atomic_store(&pub->value, (long long)nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        *tcount = (unsigned long long)tot;
+        if (a.iso_out) gb_iso_eval(a.mul, a.xcode, a.zcode, a.flip, a.a0, a.u0, a.iso_out);
+        if (a.pub) {  // hand the count to the host without a copy (gb_host_slot_wait)
+            __hip_atomic_store(&a.pub->value, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __threadfence_system();
-            __hip_atomic_store(&pub->seq, pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&a.pub->seq, a.pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+    }
+    if (a.mf_out) {
+        long long m;
+        if (gb_grid_sum(mfn, gst + GB_GRID2_OFFSET, &m)) *a.mf_out = m;
     }
 }
 
@@ -624,6 +704,8 @@ static bool idempotent_monoid(int m) {
 }
 
 static std::mutex g_dir_mu;
+static uint64_t *g_spare = nullptr;  // zeroed bitmap for the next iso SpMV's output (under g_dir_mu)
+static int64_t g_spare_words = 0;
 
 // blocks of k_iso_work the device holds at once (the work grid is sized to one wave of blocks)
 static int64_t iso_work_resident_blocks() {
@@ -663,7 +745,7 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
     T.iso = iso;
     T.bits = gb_malloc_n<uint64_t>(gb_words(n));
     T.dense = gb_malloc((iso ? 1 : n) * zs);
-    T.d_nvals = gb_malloc_n<int64_t>(1);
+    T.d_nvals = gb_malloc_n<int64_t>(2);  // [1]: next-frontier edge hint (iso path)
     if (n == 0) {
         gb_memset(T.d_nvals, 0, sizeof(int64_t));
         return;
@@ -684,12 +766,50 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
         if (iso) {
             const int64_t uw = gb_words(u.n);
             int64_t units = (nw + PULL_U - 1) / PULL_U;  // waves the pull wants
-            std::unique_lock<std::mutex> lk(g_dir_mu, std::defer_lock);
+            std::lock_guard<std::mutex> lk(g_dir_mu);  // the spare bitmap and the direction state
+            gb_iso_args args{};
+            args.rule = gb_dir_rule{mask.count, mask.comp, n, A.nvals, alpha, dir_knob == 2};
+            // the result's iso value: evaluated by the finishing block when z is x's type or bool
+            const bool eval_ok = info.zcode == info.xcode || info.zcode == GBAMD_T_BOOL;
+            if (eval_ok) {
+                args.mul = info.mul;
+                args.xcode = info.xcode;
+                args.zcode = info.zcode;
+                args.flip = flip;
+                args.a0 = av;
+                args.u0 = uv;
+                args.iso_out = T.dense;
+            }
+            args.pub = T.pub ? gb_host_slot_device(T.pub) : nullptr;
+            args.pub_seq = (long long)T.pub_seq;
+            // a zeroed output bitmap left by the previous call (push may write into it directly)
+            bool spare_taken = false;
+            if (g_spare && g_spare_words == nw) {
+                gb_free(T.bits);
+                T.bits = g_spare;
+                spare_taken = true;
+            } else if (g_spare) {
+                gb_free(g_spare);
+            }
+            g_spare = nullptr;
+            g_spare_words = 0;
+            bool need_prep = false;
             if (can_push) {
-                // prep (frontier edges -> direction, zeroed output, iso value), then one work launch
-                lk.lock();
                 units = std::max<int64_t>(units, std::max<int64_t>((Apush->nhubs + 15) / 16, (uw + 3) / 4));
-                gb_dir_rule rule{mask.count, mask.comp, n, A.nvals, alpha, dir_knob == 2};
+                if (n == u.n) {  // outputs index the same vertex space as u: they can seed the next call
+                    args.hprow = Apush->rowptr;
+                    args.mf_out = (long long *)(T.d_nvals + 1);
+                    T.hint_key = Apush->rowptr;
+                }
+                const bool hint_ok = u.mf_hint && u.hint_key == Apush->rowptr;
+                if (hint_ok && spare_taken) {
+                    args.mf_hint = u.mf_hint;  // decide in the work kernel: one launch
+                } else {
+                    need_prep = true;
+                }
+            }
+            if (need_prep || (!eval_ok && can_push)) {
+                // prep (frontier edges -> direction, zeroed output, iso value), then the work launch
                 int64_t pcap = gb_knob("prep_grid");
                 if (pcap <= 0) pcap = 1024;
                 const unsigned prep_grid =
@@ -698,15 +818,16 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
                     hipLaunchKernelGGL((k_dir_prep<SRT, X, Z, true>), dim3(prep_grid), dim3(SPMV_BLOCK), 0,
                                        gb_stream(), srf, u.bits, uw, Apush->rowptr, gst, dst, T.bits, nw,
                                        (unsigned long long *)T.d_nvals, (const X *)av, (const X *)uv, (Z *)T.dense,
-                                       rule);
+                                       args.rule);
                 else
                     hipLaunchKernelGGL((k_dir_prep<SRT, X, Z, false>), dim3(prep_grid), dim3(SPMV_BLOCK), 0,
                                        gb_stream(), srf, u.bits, uw, Apush->rowptr, gst, dst, T.bits, nw,
                                        (unsigned long long *)T.d_nvals, (const X *)av, (const X *)uv, (Z *)T.dense,
-                                       rule);
+                                       args.rule);
                 GB_LAUNCH_CHECK();
-            } else {
-                gb_memset(T.d_nvals, 0, sizeof(int64_t));
+                args.mf_hint = nullptr;
+                args.dst = dst;
+            } else if (!eval_ok) {
                 if (flip)
                     hipLaunchKernelGGL((k_iso_value<SRT, X, Z, true>), dim3(1), dim3(1), 0, gb_stream(), srf,
                                        (const X *)av, (const X *)uv, (Z *)T.dense);
@@ -715,6 +836,10 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
                                        (const X *)av, (const X *)uv, (Z *)T.dense);
                 GB_LAUNCH_CHECK();
             }
+            if (can_push) {  // zeroed by this launch, for the next call's push output
+                args.spare = gb_malloc_n<uint64_t>(nw);
+                args.spare_words = nw;
+            }
             int64_t gcap = gb_knob("iso_work_grid");
             if (gcap <= 0) gcap = iso_work_resident_blocks();
             const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 3) / 4, gcap));
@@ -722,9 +847,10 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
                                u.bits, can_push ? Apush->rowptr : nullptr, can_push ? Apush->colidx : nullptr,
                                can_push ? Apush->hubs : nullptr, can_push ? Apush->nhubs : 0,
                                can_push ? Apush->hub_H : 1, mask.bits, mask.comp, T.bits,
-                               (unsigned long long *)T.d_nvals, gst, can_push ? dst : nullptr,
-                               T.pub ? gb_host_slot_device(T.pub) : nullptr, (long long)T.pub_seq);
+                               (unsigned long long *)T.d_nvals, gst, args);
             GB_LAUNCH_CHECK();
+            g_spare = args.spare;
+            g_spare_words = args.spare ? nw : 0;
             T.published = T.pub != nullptr;
             return;
         }

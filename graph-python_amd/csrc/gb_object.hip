@@ -68,6 +68,8 @@ static void alloc_empty_storage(GB_Obj *A) {
         gb_memset(A->d_nvals, 0, sizeof(int64_t));
         A->nvals = 0;
         A->nvals_valid = true;
+        A->hint_valid = false;
+        A->pub_seq = 0;
     }
     A->iso = false;
 }
@@ -203,6 +205,7 @@ void gb_install_bitmap(GB_Obj *C, int64_t n, uint64_t *bits, void *dense, bool i
         }
         C->nvals_valid = false;
         C->pub_seq = 0;
+        C->hint_valid = false;
         return;
     }
     // matrix target (n x 1): bitmap -> CSR
@@ -738,6 +741,7 @@ static void vector_set_element(GB_Obj *v, T x, int64_t i) {
                        v->iso ? nullptr : (T *)v->dense, i, x, (unsigned long long *)v->d_nvals);
     GB_LAUNCH_CHECK();
     v->nvals_valid = false;
+    v->hint_valid = false;
 }
 
 template <class T>
@@ -1017,6 +1021,7 @@ static void vector_resize(GB_Obj *v, int64_t n) {
     v->iso = iso;
     gb_bitmap_count(bits, n, v->d_nvals);
     v->nvals_valid = false;
+    v->hint_valid = false;
 }
 
 // ================================================================== dup
@@ -1132,6 +1137,7 @@ GrB_Info GrB_Matrix_removeElement(GrB_Matrix A, GrB_Index i, GrB_Index j) {
                                (int64_t)i, (unsigned long long *)o->d_nvals);
             GB_LAUNCH_CHECK();
             o->nvals_valid = false;
+            o->hint_valid = false;
             return;
         }
         matrix_remove_element(o, i, j);
@@ -1353,6 +1359,7 @@ GrB_Info GxB_Vector_device_touch(GrB_Vector v) {
         GB_REQUIRE(o->kind != GB_KIND_MATRIX, GrB_INVALID_OBJECT, "not a vector");
         gb_bitmap_count(o->bits, o->nrows, o->d_nvals);
         o->nvals_valid = false;
+        o->hint_valid = false;
     });
 }
 GrB_Info GxB_Vector_bitmap_export(GrB_Vector v, void *dst, GrB_Index nwords) {
@@ -1385,6 +1392,7 @@ GrB_Info GxB_Vector_bitmap_import(GrB_Vector v, const void *src, GrB_Index nword
         o->iso = true;
         gb_bitmap_count(o->bits, o->nrows, o->d_nvals);
         o->nvals_valid = false;
+        o->hint_valid = false;
     });
 }
 GrB_Info GxB_Matrix_prepare_transpose(GrB_Matrix A) {

@@ -52,6 +52,10 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
     else gb_get_csr(av, A);
     gb_bitmap_view uv;
     gb_get_bitmap(uv, u);
+    if (u->kind != GB_KIND_MATRIX && u->hint_valid) {
+        uv.mf_hint = (const long long *)(u->d_nvals + 1);
+        uv.hint_key = u->hint_key;
+    }
     gb_vmask m;
     gb_make_vmask(m, mask, d, a_rows);
     // the other orientation (cached on matrices) enables the push direction for iso results
@@ -71,11 +75,16 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
         T.pub_seq = gb_next_pub_seq();
     }
     gb_spmv(T, av, push, uv, m, sr, vxm);
+    const void *hint_key = T.hint_key;
     const bool direct = gb_writeback_vector(w, T, mask, d, accum, true);
     if (direct && T.published) {
         // w's count is the one the kernel published; valid until more work is enqueued
         w->pub_seq = T.pub_seq;
         w->pub_epoch = gb_epoch();
+    }
+    if (direct && hint_key && w->kind != GB_KIND_MATRIX) {
+        w->hint_valid = true;
+        w->hint_key = hint_key;
     }
 }
 
@@ -547,6 +556,7 @@ static bool assign_all_scalar_fast(GB_Obj *w, GB_Obj *mask, const char *xc, cons
     });
     GB_LAUNCH_CHECK();
     w->nvals_valid = false;
+    w->hint_valid = false;
     return true;
 }
 
