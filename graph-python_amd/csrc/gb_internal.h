@@ -82,6 +82,8 @@ struct GB_Matrix_opaque {
     // gb_view_hubs (gb_mxv.hip); dropped with the transpose
     int32_t *hub_tab[2];
     int64_t hub_n[2], hub_H[2];
+    // cached bitmaps of the non-empty rows of the CSR (0) / CSC (1)
+    uint64_t *rows_ne[2];
     // ---- bitmap (kind == VECTOR / SCALAR); length n = nrows (ncols == 1)
     uint64_t *bits;      // [ceil(n/64)]
     void *dense;         // [n] or [1] when iso
@@ -213,11 +215,14 @@ struct gb_csr_view {
     // hub chunks (rows longer than hub_H cut into hub_H-edge pieces): pairs (row, piece)
     const int32_t *hubs = nullptr;
     int64_t nhubs = 0, hub_H = 0;
+    const uint64_t *nonempty = nullptr;  // bitmap of rows with entries (when attached)
     gb_scratch own;
 };
 void gb_get_csr(gb_csr_view &v, GB_Obj *A);
 // attach the cached hub-chunk table of matrix A's orientation (0 CSR, 1 CSC) to v
 void gb_view_hubs(gb_csr_view &v, GB_Obj *A, int orient, int64_t H);
+// attach the cached non-empty-rows bitmap of matrix A's orientation to v
+void gb_view_nonempty(gb_csr_view &v, GB_Obj *A, int orient);
 // CSC of A (i.e. CSR of A^T), cached on the object when A is a matrix.
 void gb_get_csc(gb_csr_view &v, GB_Obj *A);
 // Values of a CSR view cast to type `code` (returns the view's own pointer if same type).

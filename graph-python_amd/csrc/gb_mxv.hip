@@ -392,7 +392,8 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
                                                       const uint64_t *__restrict__ ubits,
                                                       const uint64_t *__restrict__ mbits, bool mcomp,
                                                       uint64_t *__restrict__ tbits, gb_wlist &L,
-                                                      const int64_t *__restrict__ hprow, long long &mfn) {
+                                                      const int64_t *__restrict__ hprow, long long &mfn,
+                                                      int p1_steps, int cap0, const uint64_t *__restrict__ rne) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -404,8 +405,13 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
         const int64_t wl = w0 + (lane & (PULL_U - 1));
         uint64_t mine = ~0ULL;
         if (mbits) mine = wl < nwords ? (mcomp ? ~mbits[wl] : mbits[wl]) : 0;
+        if (rne && wl < nwords) mine &= rne[wl];  // rows without entries produce nothing
         if (wl == nwords - 1) mine &= tail;
         if (wl >= nwords) mine = 0;
+        if (!__ballot(mine != 0)) {  // nothing open in these words
+            if (lane < PULL_U && wl < nwords) tbits[wl] = 0;
+            continue;
+        }
         bool live[PULL_U], found[PULL_U];
         int64_t p[PULL_U], p1[PULL_U];
         // row bounds are loaded for every row, independently of the mask word
@@ -425,7 +431,7 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
             found[u] = false;
             dg[u] = (int32_t)(p1[u] - p[u]);
         }
-        for (int it = 0; it < 2; it++) {
+        for (int it = 0; it < p1_steps; it++) {
             bool go[PULL_U], any = false;
 #pragma unroll
             for (int u = 0; u < PULL_U; u++) {
@@ -472,7 +478,7 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
         unsigned long long hitw[PULL_U];
 #pragma unroll
         for (int u = 0; u < PULL_U; u++) hitw[u] = 0;
-        int cap = 16;
+        int cap = cap0;
         while (n) {
             gb_wave_sync();
             const int total = gb_wlist_round(L, n, cap, lane);
@@ -606,6 +612,9 @@ struct gb_iso_args {
     // a bitmap to zero for the next call's push output
     uint64_t *spare;
     int64_t spare_words;
+    // pull shape: lane-per-row steps of 4 edges, then the first per-row cap of the list rounds
+    int p1_steps, cap0;
+    const uint64_t *rows_nonempty;  // pull rows with entries (nullptr: all)
 };
 
 // One launch does the chosen direction and finishes the result: count
@@ -631,7 +640,8 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
         cnt = gb_push_phase(nwords_u, ubits, prow, pcol, hubs, nhubs, H, mbits, mcomp,
                             (unsigned long long *)tbits, L, a.hprow, mfn);
     else
-        cnt = gb_pull_iso_phase(nrows, rowptr, colidx, ubits, mbits, mcomp, tbits, L, a.hprow, mfn);
+        cnt = gb_pull_iso_phase(nrows, rowptr, colidx, ubits, mbits, mcomp, tbits, L, a.hprow, mfn, a.p1_steps,
+                                a.cap0, a.rows_nonempty);
     long long tot;
     if (gb_grid_sum(cnt, gst, &tot)) {
         *tcount = (unsigned long long)tot;
@@ -689,6 +699,30 @@ void gb_view_hubs(gb_csr_view &v, GB_Obj *A, int orient, int64_t H) {
     v.hubs = A->hub_tab[orient];
     v.nhubs = A->hub_n[orient];
     v.hub_H = H;
+}
+
+__global__ void k_rows_nonempty(const int64_t *__restrict__ rowptr, int64_t n, uint64_t *__restrict__ ne) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (n + 63) >> 6;
+    for (int64_t w = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; w < nw;
+         w += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+        const int64_t r = (w << 6) + lane;
+        const unsigned long long b = __ballot(r < n && rowptr[r + 1] > rowptr[r]);
+        if (lane == 0) ne[w] = b;
+    }
+}
+
+void gb_view_nonempty(gb_csr_view &v, GB_Obj *A, int orient) {
+    if (A->kind != GB_KIND_MATRIX) return;
+    if (!A->rows_ne[orient]) {
+        const int64_t nw = gb_words(v.nrows);
+        A->rows_ne[orient] = gb_malloc_n<uint64_t>(nw);
+        const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nw + 3) / 4, 8192));
+        hipLaunchKernelGGL(k_rows_nonempty, dim3(g), dim3(256), 0, gb_stream(), v.rowptr, v.nrows,
+                           A->rows_ne[orient]);
+        GB_LAUNCH_CHECK();
+    }
+    v.nonempty = A->rows_ne[orient];
 }
 
 // constant value of an iso result: mult(a0, u0) (positional ops are never iso)
@@ -769,6 +803,11 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             std::lock_guard<std::mutex> lk(g_dir_mu);  // the spare bitmap and the direction state
             gb_iso_args args{};
             args.rule = gb_dir_rule{mask.count, mask.comp, n, A.nvals, alpha, dir_knob == 2};
+            args.p1_steps = (int)gb_knob("pull_steps");
+            if (args.p1_steps <= 0) args.p1_steps = 2;
+            args.cap0 = (int)gb_knob("pull_cap");
+            if (args.cap0 <= 0) args.cap0 = 16;
+            args.rows_nonempty = A.nonempty;
             // the result's iso value: evaluated by the finishing block when z is x's type or bool
             const bool eval_ok = info.zcode == info.xcode || info.zcode == GBAMD_T_BOOL;
             if (eval_ok) {

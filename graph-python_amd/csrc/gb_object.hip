@@ -118,6 +118,8 @@ void gb_drop_transpose(GB_Obj *A) {
         gb_free(A->hub_tab[o]);
         A->hub_tab[o] = nullptr;
         A->hub_n[o] = A->hub_H[o] = 0;
+        gb_free(A->rows_ne[o]);
+        A->rows_ne[o] = nullptr;
     }
 }
 

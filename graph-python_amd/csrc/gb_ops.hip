@@ -50,6 +50,7 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
     gb_csr_view av, pv;
     if (use_csc) gb_get_csc(av, A);
     else gb_get_csr(av, A);
+    gb_view_nonempty(av, A, use_csc ? 1 : 0);
     gb_bitmap_view uv;
     gb_get_bitmap(uv, u);
     if (u->kind != GB_KIND_MATRIX && u->hint_valid) {
