@@ -54,6 +54,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    # rehearsal of the N>1 path on one GPU: all ranks on one device, gloo transport
+    p.add_argument("--dist-backend", default="nccl")
+    p.add_argument("--device", type=int, default=None, help="override LOCAL_RANK's device")
     return p.parse_args()
 
 
@@ -91,6 +94,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.device is not None:
+        local_rank = args.device
     import torch
 
     dist = None
@@ -98,7 +103,10 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(args.dist_backend)
     os.environ["GRAPHBLAS_AMD_DEVICE"] = str(local_rank)
     import graphblas_amd as gb
     import oracle as O
@@ -108,11 +116,11 @@ def main():
     stream = torch.cuda.Stream()
     gb.set_stream(stream)
 
+    from graphblas_amd import dist as gdist
+
     scale, n = args.scale, 1 << args.scale
-    words = (n + 63) // 64
-    slot = (words + world - 1) // world          # bitmap words per rank (equal, padded)
-    lo_w, hi_w = min(words, rank * slot), min(words, (rank + 1) * slot)
-    lo, hi = lo_w * 64, min(n, hi_w * 64)
+    part = gdist.partition(n, world, rank)  # equal 64-aligned bitmap-word slots per rank
+    words, lo_w, hi_w, lo, hi = part["words"], part["lo_w"], part["hi_w"], part["lo"], part["hi"]
     nloc = hi - lo
 
     # ---------------- graph (ingest, untimed)
@@ -154,8 +162,7 @@ def main():
     ok(lib.GrB_Vector_new(ctypes.byref(v), lib.GrB_INT32, nloc), "v")
     if world > 1:
         ok(lib.GrB_Vector_new(ctypes.byref(qloc), lib.GrB_BOOL, nloc), "qloc")
-        gath = torch.zeros(slot * world, dtype=torch.int64, device="cuda")
-        send = torch.zeros(slot, dtype=torch.int64, device="cuda")
+        exchange = gdist.BitmapAllGather(dist, part, world, "cuda")
     nv = ctypes.c_uint64()
     ev_pairs, level_counts = [], []
 
@@ -196,9 +203,10 @@ def main():
                     e1.record(stream)
                     ev_pairs.append((e0, e1))
                 # exchange: all-gather the frontier bitmap over RCCL (stream-ordered)
-                ok(lib.GxB_Vector_bitmap_export(qloc, ctypes.c_void_p(send.data_ptr()), hi_w - lo_w), "bm out")
+                ok(lib.GxB_Vector_bitmap_export(qloc, ctypes.c_void_p(exchange.send.data_ptr()), hi_w - lo_w),
+                   "bm out")
                 with torch.cuda.stream(stream):
-                    dist.all_gather_into_tensor(gath, send)
+                    gath = exchange.run()
                 ok(lib.GxB_Vector_bitmap_import(q, ctypes.c_void_p(gath.data_ptr()), words), "bm in")
             ok(lib.GrB_Vector_nvals(ctypes.byref(nv), q), "nvals")
             if nv.value == 0:
@@ -230,6 +238,19 @@ def main():
             parity = bool(np.array_equal(got, lev_ref))
             if not parity:
                 raise SystemExit("BFS parity failure vs oracle")
+        elif k == 0:
+            # sharded run: gather every rank's level slice, rank 0 checks against the oracle
+            dev = "cuda" if args.dist_backend == "nccl" else "cpu"
+            mine = torch.zeros(part["slot"] * 64, dtype=torch.int32)
+            mine[torch.from_numpy(idx.astype(np.int64))] = torch.from_numpy(lv)
+            allv = [torch.zeros_like(mine).to(dev) for _ in range(world)]
+            dist.all_gather(allv, mine.to(dev))
+            if rank == 0:
+                got = torch.cat([t.cpu() for t in allv]).numpy()[:n]
+                lev_ref, _, _ = O.bfs_levels(O.rmat(scale, args.edge_factor, args.seed), int(src))
+                parity = bool(np.array_equal(got, lev_ref))
+                if not parity:
+                    raise SystemExit("sharded BFS parity failure vs oracle")
     level_counts.clear()
 
     for w in range(args.warmup):

@@ -1,0 +1,111 @@
+"""Sharded BFS exchange logic at world_size 2 on CPU (gloo): the partition and
+bitmap all-gather of graphblas_amd.dist, with a numpy local step over each
+rank's row shard of A^T, must reproduce the oracle's BFS levels.
+The GPU run uses the same partition and exchange with GrB_mxv as the local step
+and RCCL as the transport (bench.py)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle as O
+from graphblas_amd import dist as gdist
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class _Csr:
+    def __init__(self, indptr, indices):
+        self.indptr, self.indices = indptr, indices
+
+
+def _transpose(G):
+    rows = np.repeat(np.arange(G.nrows), np.diff(G.indptr))
+    order = np.lexsort((rows, G.indices))
+    indptr = np.zeros(G.ncols + 1, np.int64)
+    np.cumsum(np.bincount(G.indices, minlength=G.ncols), out=indptr[1:])
+    return _Csr(indptr, rows[order])
+
+
+def _worker(rank, world, port, scale, src, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    G = O.rmat(scale, 16, 42)
+    n = G.nrows
+    AT = _transpose(G)  # rows of A^T = in-edges: pull mxv, as in bench.py
+    part = gdist.partition(n, world, rank)
+    lo, hi = part["lo"], part["hi"]
+    ex = gdist.BitmapAllGather(dist, part, world, "cpu")
+    frontier = np.zeros(n, bool)
+    frontier[src] = True
+    visited = np.zeros(hi - lo, bool)
+    level = np.zeros(hi - lo, np.int32)
+    d = 0
+    while True:
+        d += 1
+        loc = frontier[lo:hi]
+        level[loc & ~visited] = d
+        visited |= loc
+        # q_r<!v_r.S, replace> = A^T_r lor.land q  (pull over the shard's rows)
+        nxt = np.zeros(hi - lo, bool)
+        for r in range(lo, hi):
+            if visited[r - lo]:
+                continue
+            cols = AT.indices[AT.indptr[r]:AT.indptr[r + 1]]
+            nxt[r - lo] = bool(frontier[cols].any())
+        ex.send.copy_(torch.from_numpy(gdist.pack_bits(nxt, part["slot"])))
+        full = ex.run().numpy()
+        # words are slot-aligned per rank: rank k's slice starts at word k*slot
+        frontier = np.zeros(n, bool)
+        for k in range(world):
+            pk = gdist.partition(n, world, k)
+            sl = full[k * part["slot"]:k * part["slot"] + (pk["hi_w"] - pk["lo_w"])]
+            frontier[pk["lo"]:pk["hi"]] = gdist.unpack_bits(sl, pk["hi"] - pk["lo"])
+        if not frontier.any():
+            break
+    out_q.put((rank, lo, hi, level))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("scale", [8, 10])
+def test_sharded_bfs_world2_matches_oracle(scale):
+    world = 2
+    G = O.rmat(scale, 16, 42)
+    src = int(np.argmax(np.diff(G.indptr)))
+    ref, _, _ = O.bfs_levels(G, src)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, scale, src, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = np.zeros(G.nrows, np.int32)
+    for _ in range(world):
+        rank, lo, hi, level = q.get(timeout=120)
+        got[lo:hi] = level
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert np.array_equal(got, ref)
+
+
+def test_partition_covers_vertices():
+    for n in [1, 63, 64, 65, 1000, 4096 + 7]:
+        for world in [1, 2, 3, 8]:
+            parts = [gdist.partition(n, world, r) for r in range(world)]
+            covered = np.zeros(n, int)
+            for p in parts:
+                covered[p["lo"]:p["hi"]] += 1
+                assert p["lo"] % 64 == 0 and p["hi_w"] - p["lo_w"] <= p["slot"]
+            assert (covered == 1).all()
