@@ -40,6 +40,10 @@ class BitmapAllGather:
     def run(self):
         if self._fused:
             self.dist.all_gather_into_tensor(self.gathered, self.send)
+        elif self.send.is_cuda:  # gloo rehearsal of the GPU path: stage through host memory
+            host = self.gathered.cpu()
+            self.dist.all_gather(list(host.chunk(self.world)), self.send.cpu())
+            self.gathered.copy_(host)
         else:
             self.dist.all_gather(list(self.gathered.chunk(self.world)), self.send)
         return self.gathered
