@@ -373,6 +373,48 @@ GB_DEV T gb_shfl_xor(T v, int mask, int width) {
     }
 }
 
+template <class T>
+GB_DEV T gb_shfl_up(T v, int delta, int width) {
+    if constexpr (sizeof(T) == 8) {
+        int64_t x;
+        __builtin_memcpy(&x, &v, 8);
+        int lo = __shfl_up((int)(x & 0xffffffff), delta, width);
+        int hi = __shfl_up((int)(x >> 32), delta, width);
+        int64_t y = ((int64_t)(uint32_t)lo) | ((int64_t)hi << 32);
+        T r;
+        __builtin_memcpy(&r, &y, 8);
+        return r;
+    } else {
+        int x = 0;
+        __builtin_memcpy(&x, &v, sizeof(T));
+        x = __shfl_up(x, delta, width);
+        T r;
+        __builtin_memcpy(&r, &x, sizeof(T));
+        return r;
+    }
+}
+
+template <class T>
+GB_DEV T gb_shfl_down(T v, int delta, int width) {
+    if constexpr (sizeof(T) == 8) {
+        int64_t x;
+        __builtin_memcpy(&x, &v, 8);
+        int lo = __shfl_down((int)(x & 0xffffffff), delta, width);
+        int hi = __shfl_down((int)(x >> 32), delta, width);
+        int64_t y = ((int64_t)(uint32_t)lo) | ((int64_t)hi << 32);
+        T r;
+        __builtin_memcpy(&r, &y, 8);
+        return r;
+    } else {
+        int x = 0;
+        __builtin_memcpy(&x, &v, sizeof(T));
+        x = __shfl_down(x, delta, width);
+        T r;
+        __builtin_memcpy(&r, &x, sizeof(T));
+        return r;
+    }
+}
+
 GB_DEV bool gb_bit(const uint64_t *bits, int64_t i) { return (bits[i >> 6] >> (i & 63)) & 1ULL; }
 
 // (bool) of one value of runtime type `code` (mask semantics: -0.0 is false, NaN true)

@@ -84,6 +84,9 @@ struct GB_Matrix_opaque {
     int64_t hub_n[2], hub_H[2];
     // cached bitmaps of the non-empty rows of the CSR (0) / CSC (1)
     uint64_t *rows_ne[2];
+    // cached long-row chunk tables (general SpMV, gb_mxv.hip)
+    int32_t *long_tab[2];
+    int64_t long_n[2];
     // ---- bitmap (kind == VECTOR / SCALAR); length n = nrows (ncols == 1)
     uint64_t *bits;      // [ceil(n/64)]
     void *dense;         // [n] or [1] when iso
@@ -216,6 +219,8 @@ struct gb_csr_view {
     const int32_t *hubs = nullptr;
     int64_t nhubs = 0, hub_H = 0;
     const uint64_t *nonempty = nullptr;  // bitmap of rows with entries (when attached)
+    const int32_t *lchunks = nullptr;    // long-row chunks (row, piece) of the general SpMV (when attached)
+    int64_t nlchunks = -1;
     gb_scratch own;
 };
 void gb_get_csr(gb_csr_view &v, GB_Obj *A);
@@ -223,6 +228,7 @@ void gb_get_csr(gb_csr_view &v, GB_Obj *A);
 void gb_view_hubs(gb_csr_view &v, GB_Obj *A, int orient, int64_t H);
 // attach the cached non-empty-rows bitmap of matrix A's orientation to v
 void gb_view_nonempty(gb_csr_view &v, GB_Obj *A, int orient);
+void gb_view_long_rows(gb_csr_view &v, GB_Obj *A, int orient);
 // CSC of A (i.e. CSR of A^T), cached on the object when A is a matrix.
 void gb_get_csc(gb_csr_view &v, GB_Obj *A);
 // Values of a CSR view cast to type `code` (returns the view's own pointer if same type).

@@ -48,29 +48,45 @@ __global__ __launch_bounds__(MXM_BLOCK) void k_dot_masked(
     MXM_STRIDE(q, nm) {
         const int64_t i = mrowof[q];
         const int32_t j = mci[q];
-        int64_t pa = arp[i], ea = arp[i + 1], pb = brp[j], eb = brp[j + 1];
+        const int64_t pa0 = arp[i], ea = arp[i + 1], pb0 = brp[j], eb = brp[j + 1];
+        // walk the shorter list in ascending k; find each k in the longer one by
+        // galloping from the last match (exponential then binary search)
+        const bool a_short = (ea - pa0) <= (eb - pb0);
+        const int32_t *__restrict__ sci = a_short ? aci : bci;
+        const int32_t *__restrict__ lci = a_short ? bci : aci;
+        int64_t ps = a_short ? pa0 : pb0, es = a_short ? ea : eb;
+        int64_t pl = a_short ? pb0 : pa0, el = a_short ? eb : ea;
         bool found = false;
         Z acc = Z();
-        while (pa < ea && pb < eb) {
-            int32_t ka = aci[pa], kb = bci[pb];
-            if (ka < kb) {
-                // gallop in A when it is far behind
-                pa++;
-            } else if (kb < ka) {
-                pb++;
-            } else {
-                X a = X(), b = X();
-                if (SR::reads_values && avx && bvx) {
-                    a = avx[a_iso ? 0 : pa];
-                    b = bvx[b_iso ? 0 : pb];
+        for (; ps < es && pl < el; ps++) {
+            const int32_t k = sci[ps];
+            if (lci[pl] < k) {
+                int64_t lo = pl, step = 1;  // lci[lo] < k
+                while (lo + step < el && lci[lo + step] < k) {
+                    lo += step;
+                    step <<= 1;
                 }
-                Z z = sr.mult(a, b, i, ka, j);
-                acc = found ? sr.add(acc, z) : z;
-                found = true;
-                if (sr.terminal(acc)) break;
-                pa++;
-                pb++;
+                int64_t hi = lo + step < el ? lo + step : el;  // lci[hi] >= k or hi == el
+                while (hi - lo > 1) {
+                    const int64_t mid = (lo + hi) >> 1;
+                    if (lci[mid] < k) lo = mid;
+                    else hi = mid;
+                }
+                pl = hi;
+                if (pl >= el) break;
             }
+            if (lci[pl] != k) continue;
+            const int64_t pa = a_short ? ps : pl, pb = a_short ? pl : ps;
+            X a = X(), b = X();
+            if (SR::reads_values && avx && bvx) {
+                a = avx[a_iso ? 0 : pa];
+                b = bvx[b_iso ? 0 : pb];
+            }
+            Z z = sr.mult(a, b, i, k, j);
+            acc = found ? sr.add(acc, z) : z;
+            found = true;
+            if (sr.terminal(acc)) break;
+            pl++;
         }
         tflag[q] = found ? 1 : 0;
         if (found) tval[q] = acc;

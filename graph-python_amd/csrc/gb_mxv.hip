@@ -617,6 +617,199 @@ struct gb_iso_args {
     const uint64_t *rows_nonempty;  // pull rows with entries (nullptr: all)
 };
 
+// ------------------------------------------------ general SpMV: balanced words
+// One wave per 64-row output word (a bitmap word): the entries of the word's
+// rows (rows of at most LONG entries) are concatenated and walked 256 at a
+// time, four independent gathers per lane; products of one row sit in
+// consecutive lanes, so a segmented scan across the wave folds them and the
+// last lane of each segment adds the run to the row's accumulator in LDS (row
+// order = ascending k: deterministic).  Rows longer than LONG are cut into
+// CH-entry chunks (a table cached on the matrix) whose partial folds are
+// combined in chunk order by k_spmv_fold.
+#define SPMV_LONG 128
+#define SPMV_CH 1024
+
+template <class SR, class X, class Z, bool FLIP>
+__device__ __forceinline__ void gb_spmv_product(SR &sr, bool rv, const X *__restrict__ avals, bool a_iso, X a0,
+                                                const X *__restrict__ uvals, bool u_iso, X u0, int64_t p, int k,
+                                                int64_t r, Z &z) {
+    X a = X(), b = X();
+    if (rv) {
+        a = a_iso ? a0 : avals[p];
+        b = u_iso ? u0 : uvals[k];
+    }
+    z = FLIP ? sr.mult(b, a, 0, k, r) : sr.mult(a, b, r, k, 0);
+}
+
+template <class SR, class X, class Z, bool FLIP>
+__global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
+    SR sr, int64_t nrows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ colidx,
+    const X *__restrict__ avals, bool a_iso, const uint64_t *__restrict__ ubits,
+    const X *__restrict__ uvals, bool u_iso, const uint64_t *__restrict__ mbits, bool mcomp,
+    const int32_t *__restrict__ chunks, int64_t nchunks, Z *__restrict__ cpart, int8_t *__restrict__ cfound,
+    uint64_t *__restrict__ tbits, Z *__restrict__ tvals, unsigned long long *__restrict__ tcount,
+    unsigned long long *__restrict__ gst) {
+    __shared__ Z accs[WAVES_PER_BLOCK][64];
+    __shared__ int fls[WAVES_PER_BLOCK][64];
+    Z *acc = accs[threadIdx.x >> 6];
+    int *fl = fls[threadIdx.x >> 6];  // row has at least one product
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const int64_t nwords = (nrows + 63) >> 6;
+    const bool rv = SR::reads_values && avals && uvals;
+    X a0 = X(), u0 = X();
+    if (rv) {
+        if (a_iso) a0 = avals[0];
+        if (u_iso) u0 = uvals[0];
+    }
+    fl[lane] = 0;
+    gb_wave_sync();
+    long long cnt = 0;
+    // long-row chunks: lane-sequential folds in ascending k, then a wave fold in lane order
+    for (int64_t c = wave; c < nchunks; c += nwaves) {
+        const int64_t r = chunks[2 * c], piece = chunks[2 * c + 1];
+        bool f = false;
+        Z z = Z();
+        if (!mbits || gb_bit(mbits, r) != mcomp) {
+            const int64_t pe = rowptr[r + 1];
+            const int64_t p0 = rowptr[r] + piece * SPMV_CH;
+            const int64_t p1 = p0 + SPMV_CH < pe ? p0 + SPMV_CH : pe;
+            for (int64_t q = p0 + lane; q < p1; q += 256) {
+                int kk[4];
+                bool ok[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    ok[u] = q + 64 * u < p1;
+                    kk[u] = ok[u] ? colidx[q + 64 * u] : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (!ok[u] || !gb_bit(ubits, kk[u])) continue;
+                    Z t;
+                    gb_spmv_product<SR, X, Z, FLIP>(sr, rv, avals, a_iso, a0, uvals, u_iso, u0, q + 64 * u, kk[u],
+                                                    r, t);
+                    z = f ? sr.add(z, t) : t;
+                    f = true;
+                }
+            }
+        }
+        for (int off = 1; off < 64; off <<= 1) {  // fold lanes in order: lane l absorbs l+off
+            const bool of = __shfl_down((int)f, off, 64);
+            const Z oz = gb_shfl_down(z, off, 64);
+            if (lane + off < 64 && (lane & (2 * off - 1)) == 0 && of) {
+                z = f ? sr.add(z, oz) : oz;
+                f = true;
+            }
+        }
+        if (lane == 0) {
+            cfound[c] = f ? 1 : 0;
+            if (f) cpart[c] = z;
+        }
+    }
+    // output words
+    for (int64_t w = wave; w < nwords; w += nwaves) {
+        const int64_t r = (w << 6) + lane;
+        bool open = r < nrows;
+        if (open && mbits) open = gb_bit(mbits, r) != mcomp;
+        int64_t p0 = 0;
+        int len = 0;
+        if (open) {
+            p0 = rowptr[r];
+            const int64_t d = rowptr[r + 1] - p0;
+            len = d > SPMV_LONG ? 0 : (int)d;  // long rows: chunks + k_spmv_fold
+        }
+        int incl = len;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += y;
+        }
+        const int excl = incl - len;
+        const int total = __shfl(incl, 63, 64);
+        for (int e0 = 0; e0 < total; e0 += 256) {
+            int k[4], own[4];
+            int64_t pos[4];
+            bool ok[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int e = e0 + lane + 64 * u;
+                int lo = 0;
+#pragma unroll
+                for (int st = 32; st > 0; st >>= 1)
+                    if (__shfl(incl, lo + st - 1, 64) <= e) lo += st;
+                own[u] = lo;
+                pos[u] = __shfl(p0, lo, 64) + (e - __shfl(excl, lo, 64));
+                ok[u] = e < total;
+                k[u] = ok[u] ? colidx[pos[u]] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                bool f = ok[u] && gb_bit(ubits, k[u]);
+                Z z = Z();
+                if (f)
+                    gb_spmv_product<SR, X, Z, FLIP>(sr, rv, avals, a_iso, a0, uvals, u_iso, u0, pos[u], k[u],
+                                                    (w << 6) + own[u], z);
+                // segmented inclusive scan over lanes of the same row
+                const int row = ok[u] ? own[u] : 64 + lane;  // idle lanes: own segment
+                for (int off = 1; off < 64; off <<= 1) {
+                    const int orow = __shfl_up(row, off, 64);
+                    const bool of = __shfl_up((int)f, off, 64);
+                    const Z oz = gb_shfl_up(z, off, 64);
+                    if (lane >= off && orow == row && of) {
+                        z = f ? sr.add(oz, z) : oz;
+                        f = true;
+                    }
+                }
+                const int nrow = __shfl_down(row, 1, 64);
+                const bool last = ok[u] && (lane == 63 || nrow != row);
+                // a row's runs arrive in order (earlier batches first): fold into its accumulator
+                if (last && f) {
+                    acc[row] = fl[row] ? sr.add(acc[row], z) : z;
+                    fl[row] = 1;
+                }
+                gb_wave_sync();
+            }
+        }
+        const bool hit = fl[lane] != 0;
+        const unsigned long long fmask = __ballot(hit);
+        if (hit) tvals[r] = acc[lane];
+        if (lane == 0) {
+            tbits[w] = fmask;
+            cnt += __popcll(fmask);
+        }
+        fl[lane] = 0;
+        gb_wave_sync();
+    }
+    long long tot;
+    if (gb_grid_sum(cnt, gst, &tot)) *tcount = (unsigned long long)tot;  // k_spmv_fold adds the long rows
+}
+
+// long rows: fold their chunks' partials in chunk order (one thread per row)
+template <class SR, class Z>
+__global__ void k_spmv_fold(SR sr, const int32_t *__restrict__ chunks, int64_t nchunks, const Z *__restrict__ cpart,
+                            const int8_t *__restrict__ cfound, uint64_t *__restrict__ tbits, Z *__restrict__ tvals,
+                            unsigned long long *__restrict__ tcount, unsigned long long *__restrict__ gst) {
+    long long cnt = 0;
+    for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < nchunks;
+         c += (int64_t)gridDim.x * blockDim.x) {
+        if (chunks[2 * c + 1] != 0) continue;
+        const int64_t r = chunks[2 * c];
+        bool f = false;
+        Z z = Z();
+        for (int64_t h = c; h < nchunks && chunks[2 * h] == r; h++) {
+            if (!cfound[h]) continue;
+            z = f ? sr.add(z, cpart[h]) : cpart[h];
+            f = true;
+        }
+        if (f) {
+            tvals[r] = z;
+            atomicOr((unsigned long long *)&tbits[r >> 6], 1ULL << (r & 63));
+            cnt++;
+        }
+    }
+    gb_grid_add(cnt, tcount, gst);
+}
+
 // One launch does the chosen direction and finishes the result: count
 // (stored, no prior zeroing needed), next-frontier hint, iso value, mailbox.
 __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
@@ -659,10 +852,11 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
 }
 
 // hub-chunk table of a CSR: pieces per row, then (row, piece) pairs
-__global__ void k_hub_count(const int64_t *__restrict__ rowptr, int64_t n, int64_t H, int64_t *__restrict__ cnt) {
+__global__ void k_hub_count(const int64_t *__restrict__ rowptr, int64_t n, int64_t thresh, int64_t H,
+                            int64_t *__restrict__ cnt) {
     for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
         const int64_t d = rowptr[r + 1] - rowptr[r];
-        cnt[r] = d > H ? (d + H - 1) / H : 0;
+        cnt[r] = d > thresh ? (d + H - 1) / H : 0;
     }
 }
 __global__ void k_hub_fill(const int64_t *__restrict__ cnt, const int64_t *__restrict__ off, int64_t n,
@@ -676,29 +870,41 @@ __global__ void k_hub_fill(const int64_t *__restrict__ cnt, const int64_t *__res
     }
 }
 
+// (row, piece) table of the rows of v longer than thresh, cut into H-entry pieces
+static int32_t *gb_build_chunk_table(const gb_csr_view &v, int64_t thresh, int64_t H, int64_t *total_out) {
+    const int64_t n = v.nrows;
+    gb_scratch s;
+    int64_t *cnt = s.get<int64_t>(n + 1);
+    int64_t *off = s.get<int64_t>(n + 1);
+    const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
+    hipLaunchKernelGGL(k_hub_count, dim3(g), dim3(256), 0, gb_stream(), v.rowptr, n, thresh, H, cnt);
+    GB_LAUNCH_CHECK();
+    gb_exclusive_scan_i64(cnt, off, n);
+    const int64_t total = gb_read_i64(off + n);
+    int32_t *tab = gb_malloc_n<int32_t>(2 * total + 2);
+    hipLaunchKernelGGL(k_hub_fill, dim3(g), dim3(256), 0, gb_stream(), cnt, off, n, tab);
+    GB_LAUNCH_CHECK();
+    *total_out = total;
+    return tab;
+}
+
 void gb_view_hubs(gb_csr_view &v, GB_Obj *A, int orient, int64_t H) {
     if (A->kind != GB_KIND_MATRIX) return;
     if (!A->hub_tab[orient] || A->hub_H[orient] != H) {
         gb_free(A->hub_tab[orient]);
-        A->hub_tab[orient] = nullptr;
-        const int64_t n = v.nrows;
-        gb_scratch s;
-        int64_t *cnt = s.get<int64_t>(n + 1);
-        int64_t *off = s.get<int64_t>(n + 1);
-        const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
-        hipLaunchKernelGGL(k_hub_count, dim3(g), dim3(256), 0, gb_stream(), v.rowptr, n, H, cnt);
-        GB_LAUNCH_CHECK();
-        gb_exclusive_scan_i64(cnt, off, n);
-        const int64_t total = gb_read_i64(off + n);
-        A->hub_tab[orient] = gb_malloc_n<int32_t>(2 * total + 2);
-        hipLaunchKernelGGL(k_hub_fill, dim3(g), dim3(256), 0, gb_stream(), cnt, off, n, A->hub_tab[orient]);
-        GB_LAUNCH_CHECK();
-        A->hub_n[orient] = total;
+        A->hub_tab[orient] = gb_build_chunk_table(v, H, H, &A->hub_n[orient]);
         A->hub_H[orient] = H;
     }
     v.hubs = A->hub_tab[orient];
     v.nhubs = A->hub_n[orient];
     v.hub_H = H;
+}
+
+void gb_view_long_rows(gb_csr_view &v, GB_Obj *A, int orient) {
+    if (A->kind != GB_KIND_MATRIX) return;
+    if (!A->long_tab[orient]) A->long_tab[orient] = gb_build_chunk_table(v, SPMV_LONG, SPMV_CH, &A->long_n[orient]);
+    v.lchunks = A->long_tab[orient];
+    v.nlchunks = A->long_n[orient];
 }
 
 __global__ void k_rows_nonempty(const int64_t *__restrict__ rowptr, int64_t n, uint64_t *__restrict__ ne) {
@@ -893,8 +1099,34 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             T.published = T.pub != nullptr;
             return;
         }
+        if (A.nlchunks >= 0 && gb_knob("spmv_general") != 1) {
+            // general semiring: balanced words + long-row chunks (+ their fold)
+            Z *cpart = s.get<Z>(A.nlchunks + 1);
+            int8_t *cfound = s.get<int8_t>(A.nlchunks + 1);
+            const int64_t units = std::max<int64_t>(nw, A.nlchunks);
+            const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 3) / 4, 4096));
+            if (flip)
+                hipLaunchKernelGGL((k_spmv_words<SRT, X, Z, true>), dim3(grid), dim3(SPMV_BLOCK), 0, gb_stream(), srf,
+                                   n, A.rowptr, A.colidx, (const X *)av, A.iso, u.bits, (const X *)uv, u.iso,
+                                   mask.bits, mask.comp, A.lchunks, A.nlchunks, cpart, cfound, T.bits, (Z *)T.dense,
+                                   (unsigned long long *)T.d_nvals, gst);
+            else
+                hipLaunchKernelGGL((k_spmv_words<SRT, X, Z, false>), dim3(grid), dim3(SPMV_BLOCK), 0, gb_stream(),
+                                   srf, n, A.rowptr, A.colidx, (const X *)av, A.iso, u.bits, (const X *)uv, u.iso,
+                                   mask.bits, mask.comp, A.lchunks, A.nlchunks, cpart, cfound, T.bits, (Z *)T.dense,
+                                   (unsigned long long *)T.d_nvals, gst);
+            GB_LAUNCH_CHECK();
+            if (A.nlchunks > 0) {
+                const unsigned fg = (unsigned)std::max<int64_t>(1, std::min<int64_t>((A.nlchunks + 255) / 256, 1024));
+                hipLaunchKernelGGL((k_spmv_fold<SRT, Z>), dim3(fg), dim3(256), 0, gb_stream(), srf, A.lchunks,
+                                   A.nlchunks, cpart, cfound, T.bits, (Z *)T.dense, (unsigned long long *)T.d_nvals,
+                                   gst);
+                GB_LAUNCH_CHECK();
+            }
+            return;
+        }
+        // fallback (no long-row table: the operand is not a matrix object): G lanes per row
         gb_memset(T.d_nvals, 0, sizeof(int64_t));
-        // general semiring: G lanes per row, G from the average row length
         const int64_t avg = (A.nvals + n - 1) / n;
         int lg = 0;
         while (lg < 6 && (1LL << lg) < avg) lg++;

@@ -61,8 +61,9 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
     gb_make_vmask(m, mask, d, a_rows);
     // the other orientation (cached on matrices) enables the push direction for iso results
     const gb_csr_view *push = nullptr;
-    if (A->kind == GB_KIND_MATRIX && gb_knob("spmv_direction") != 1 &&
-        gb_spmv_result_iso(sr, A->iso, uv.iso, vxm)) {
+    const bool iso_result = gb_spmv_result_iso(sr, A->iso, uv.iso, vxm);
+    if (!iso_result) gb_view_long_rows(av, A, use_csc ? 1 : 0);
+    if (A->kind == GB_KIND_MATRIX && gb_knob("spmv_direction") != 1 && iso_result) {
         if (use_csc) gb_get_csr(pv, A);
         else gb_get_csc(pv, A);
         int64_t H = gb_knob("push_heavy");

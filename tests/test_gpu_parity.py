@@ -413,12 +413,65 @@ def test_random_spmv_vs_oracle(gb, name, mon, mul, dt, kind):
     if mon == "ANY":
         return
     if dt in ("FP32", "FP64") and mon in ("PLUS", "TIMES"):
-        # the pull kernel folds a row with G lanes then a butterfly, not in ascending k as the
-        # oracle does: fp sums may differ by a few ulps of the terms (|terms| ~ 1 here)
+        # the SpMV kernels fold a row by a segmented scan across lanes (long rows: per-chunk
+        # lane folds, then chunk order), not strictly in ascending k as the oracle does: fp
+        # sums may differ by a few ulps of the terms (|terms| ~ 1 here)
         np.testing.assert_allclose(gv, ref.values, rtol=1e-5 if dt == "FP32" else 1e-12,
                                    atol=1e-6 if dt == "FP32" else 1e-12)
     else:
         assert np.array_equal(gv, ref.values)
+
+
+def _skewed_csr(rng, n, dtype):
+    """rows of very different lengths: empty, short, and longer than the SpMV's
+    long-row threshold (128) and chunk (1024), so every kernel path runs."""
+    lens = rng.integers(0, 12, n)
+    lens[::17] = rng.integers(129, 3000, lens[::17].size)
+    lens[5] = n  # a full row
+    r = np.repeat(np.arange(n), lens)
+    c = np.concatenate([rng.choice(n, size=min(L, n), replace=False) for L in lens])
+    if dtype in ("FP32", "FP64"):
+        v = rng.standard_normal(r.size).astype(O.NP[dtype])
+    elif dtype == "BOOL":
+        v = rng.random(r.size) < 0.8
+    else:
+        v = rng.integers(-40, 40, r.size).astype(O.NP[dtype])
+    return O.Csr.from_coo(r, c, v, nrows=n, ncols=n, dtype=dtype)
+
+
+@pytest.mark.parametrize("name,mon,mul,dt", [s for s in SEMIRINGS if s[0] not in ("any_pair", "lor_land")])
+@pytest.mark.parametrize("udense", [True, False])
+def test_spmv_long_rows_vs_oracle(gb, name, mon, mul, dt, udense):
+    rng = np.random.default_rng(hash((name, dt, udense, "long")) % 2**32)
+    n = 3000
+    Ao = _skewed_csr(rng, n, dt)
+    if udense:
+        u = O.Vec.from_col(_rand_csr(rng, n, 1, 0.3, dt))
+        u = O.Vec(n, dt, np.arange(n), np.resize(u.values, n) if u.values.size else np.zeros(n, O.NP[dt]))
+    else:
+        u = O.Vec.from_col(_rand_csr(rng, n, 1, 0.3, dt))
+    mo = _rand_csr(rng, n, 1, 0.6, "BOOL")
+    Ag = _to_gb(gb, Ao)
+    m = O.Vec.from_col(mo)
+    ug = gb.Vector.from_coo(u.indices, u.values, dtype=dt, size=n)
+    mg = gb.Vector.from_coo(m.indices, m.values, dtype="BOOL", size=n)
+    sr = getattr(gb.semiring, name)[dt]
+    for masked in (False, True):
+        wg = gb.Vector(dt, n)
+        if masked:
+            wg(mg.S) << Ag.mxv(ug, sr)
+            ref = O.mxv(O.Vec(n, dt, [], []), Ao, u, (mon, mul, dt), mask=m, mask_struct=True)
+        else:
+            wg << ug.vxm(Ag, sr)
+            ref = O.vxm(O.Vec(n, dt, [], []), u, Ao, (mon, mul, dt))
+        gi, gv = wg.to_coo()
+        assert np.array_equal(gi.astype(np.int64), ref.indices)
+        if dt in ("FP32", "FP64") and mon in ("PLUS", "TIMES"):
+            # long rows are folded per chunk then in chunk order; |row sums| up to ~sqrt(3000)
+            np.testing.assert_allclose(gv, ref.values, rtol=1e-5 if dt == "FP32" else 1e-12,
+                                       atol=1e-3 if dt == "FP32" else 1e-10)
+        else:
+            assert np.array_equal(gv, ref.values)
 
 
 @pytest.mark.parametrize("scale", [10, 12, 14])
