@@ -52,6 +52,7 @@ def parse():
     p.add_argument("--edge-factor", type=int, default=16)
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-secondary", action="store_true", help="skip the config 2 / config 4 lines")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     # rehearsal of the N>1 path on one GPU: all ranks on one device, gloo transport
@@ -87,6 +88,134 @@ def vector_indices(lib, v):
     ok(lib.GrB_Vector_extractTuples_INT32(ctypes.c_void_p(idx.ctypes.data), ctypes.c_void_p(lv.ctypes.data),
                                           ctypes.byref(nv), v), "extract")
     return idx.astype(np.int64), lv
+
+def _time_calls(torch, stream, fn, reps):
+    """GPU time per call of fn (HIP events on the library stream, GPU kept busy ahead)."""
+    fn()
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        torch.cuda._sleep(SLEEP_CYCLES)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / 1e3 / reps
+
+
+def secondary_workloads(lib, torch, stream, O, args):
+    """SURVEY 8(d) configs 2 and 4 on one GPU, reported beside the headline BFS line:
+    * config 2's kernel: y = x plus.times A, fp64, dense x (vxm) -- on R-MAT s22 (com-Orkut is
+      not available here); parity vs scipy (fp64, rtol 1e-6);
+    * config 4: C<A.S> = A min.plus A, INT64 weights in [1,255], R-MAT s20; parity vs the oracle
+      on a sample of 256 rows (bit-exact)."""
+    import scipy.sparse as sp
+
+    out = {}
+    # ---- config 2 kernel: plus_times fp64 SpMV
+    sc = args.scale
+    n = 1 << sc
+    A = ctypes.c_void_p()
+    ok(lib.GxB_Matrix_rmat(ctypes.byref(A), sc, args.edge_factor, args.seed, 2, 2, 0, 0), "rmat fp64")
+    ok(lib.GxB_Matrix_prepare_transpose(A), "transpose")
+    nv = ctypes.c_uint64()
+    ok(lib.GrB_Matrix_nvals(ctypes.byref(nv), A), "nvals")
+    nnz = nv.value
+    xv = np.random.default_rng(1).random(n)
+    x = ctypes.c_void_p()
+    ok(lib.GrB_Vector_new(ctypes.byref(x), lib.GrB_FP64, n), "x")
+    idx = np.arange(n, dtype=np.uint64)
+    ok(lib.GrB_Vector_build_FP64(x, ctypes.c_void_p(idx.ctypes.data), ctypes.c_void_p(xv.ctypes.data), n, None),
+       "x build")
+    y = ctypes.c_void_p()
+    ok(lib.GrB_Vector_new(ctypes.byref(y), lib.GrB_FP64, n), "y")
+    sr = lib.GrB_PLUS_TIMES_SEMIRING_FP64
+    t = _time_calls(torch, stream, lambda: ok(lib.GrB_vxm(y, None, None, sr, x, A, None), "vxm"), 20)
+    ap = np.empty(n + 1, np.uint64)
+    ai = np.empty(nnz, np.uint64)
+    ax = np.empty(nnz, np.float64)
+    lens = [ctypes.c_uint64(n + 1), ctypes.c_uint64(nnz), ctypes.c_uint64(nnz)]
+    ok(lib.GrB_Matrix_export_FP64(ctypes.c_void_p(ap.ctypes.data), ctypes.c_void_p(ai.ctypes.data),
+                                  ctypes.c_void_p(ax.ctypes.data), *[ctypes.byref(v) for v in lens], 0, A), "export")
+    S = sp.csr_matrix((ax, ai.astype(np.int64), ap.astype(np.int64)), shape=(n, n))
+    ref = S.T @ xv
+    ny = ctypes.c_uint64()
+    ok(lib.GrB_Vector_nvals(ctypes.byref(ny), y), "nvals y")
+    yi = np.empty(ny.value, np.uint64)
+    yv = np.empty(ny.value, np.float64)
+    ok(lib.GrB_Vector_extractTuples_FP64(ctypes.c_void_p(yi.ctypes.data), ctypes.c_void_p(yv.ctypes.data),
+                                         ctypes.byref(ny), y), "extract y")
+    got = np.zeros(n)
+    got[yi.astype(np.int64)] = yv
+    present = np.zeros(n, bool)
+    present[yi.astype(np.int64)] = True
+    parity2 = bool(np.array_equal(present, np.diff(S.tocsc().indptr) > 0) and
+                   np.allclose(got, ref, rtol=1e-6, atol=1e-9))
+    by = 12 * nnz + 8 * (n + 1) + 16 * n
+    out["config2_spmv_plus_times_fp64"] = {
+        "workload": f"y = x plus.times A (GrB_vxm, dense fp64 x) on R-MAT s{sc} fp64 U[0,1) (com-Orkut stand-in)",
+        "nnz": nnz, "ms": t * 1e3, "gteps": nnz / t / 1e9, "alg_bytes": by, "hbm_GBs": by / t / 1e9,
+        "parity_vs_scipy": parity2}
+    for h in (A, x, y):
+        lib.GrB_Matrix_free(ctypes.byref(h))
+    # ---- config 4: masked min_plus SpGEMM on R-MAT s20
+    s4 = 20
+    n4 = 1 << s4
+    B = ctypes.c_void_p()
+    ok(lib.GxB_Matrix_rmat(ctypes.byref(B), s4, args.edge_factor, args.seed, 1, 2, 0, 0), "rmat int64")
+    ok(lib.GxB_Matrix_prepare_transpose(B), "transpose")
+    ok(lib.GrB_Matrix_nvals(ctypes.byref(nv), B), "nvals")
+    nnz4 = nv.value
+    C = ctypes.c_void_p()
+    ok(lib.GrB_Matrix_new(ctypes.byref(C), lib.GrB_INT64, n4, n4), "C")
+    sr4 = lib.GrB_MIN_PLUS_SEMIRING_INT64
+    t4 = _time_calls(torch, stream, lambda: ok(lib.GrB_mxm(C, B, None, sr4, B, B, lib.GrB_DESC_S), "mxm"), 3)
+    bp = np.empty(n4 + 1, np.uint64)
+    bi = np.empty(nnz4, np.uint64)
+    bx = np.empty(nnz4, np.int64)
+    lens = [ctypes.c_uint64(n4 + 1), ctypes.c_uint64(nnz4), ctypes.c_uint64(nnz4)]
+    ok(lib.GrB_Matrix_export_INT64(ctypes.c_void_p(bp.ctypes.data), ctypes.c_void_p(bi.ctypes.data),
+                                   ctypes.c_void_p(bx.ctypes.data), *[ctypes.byref(v) for v in lens], 0, B),
+       "export B")
+    bp, bi = bp.astype(np.int64), bi.astype(np.int64)
+    ok(lib.GrB_Matrix_nvals(ctypes.byref(nv), C), "nvals C")
+    nnzc = nv.value
+    cp = np.empty(n4 + 1, np.uint64)
+    ci = np.empty(nnzc, np.uint64)
+    cx = np.empty(nnzc, np.int64)
+    lens = [ctypes.c_uint64(n4 + 1), ctypes.c_uint64(nnzc), ctypes.c_uint64(nnzc)]
+    ok(lib.GrB_Matrix_export_INT64(ctypes.c_void_p(cp.ctypes.data), ctypes.c_void_p(ci.ctypes.data),
+                                   ctypes.c_void_p(cx.ctypes.data), *[ctypes.byref(v) for v in lens], 0, C),
+       "export C")
+    cp = cp.astype(np.int64)
+    dout = np.diff(bp)
+    din = np.bincount(bi, minlength=n4)
+    work = int((np.repeat(dout, dout) + din[bi]).sum())
+    # oracle on 256 sampled rows: C[rows] <A[rows].S> = A[rows] min.+ A
+    rows = np.sort(np.random.default_rng(7).choice(n4, 256, replace=False))
+    sub_p = np.concatenate([[0], np.cumsum(dout[rows])])
+    sub_i = np.concatenate([bi[bp[r]:bp[r + 1]] for r in rows])
+    sub_x = np.concatenate([bx[bp[r]:bp[r + 1]] for r in rows])
+    Asub = O.Csr(len(rows), n4, "INT64", sub_p, sub_i, sub_x)
+    Afull = O.Csr(n4, n4, "INT64", bp, bi, bx)
+    ref4 = O.mxm(O.Csr.empty(len(rows), n4, "INT64"), Asub, Afull, ("MIN", "PLUS", "INT64"), mask=Asub,
+                 mask_struct=True)
+    gsub_p = np.concatenate([[0], np.cumsum(np.diff(cp)[rows])])
+    gsub_i = np.concatenate([ci[cp[r]:cp[r + 1]] for r in rows]).astype(np.int64)
+    gsub_x = np.concatenate([cx[cp[r]:cp[r + 1]] for r in rows])
+    parity4 = bool(np.array_equal(gsub_p, ref4.indptr) and np.array_equal(gsub_i, ref4.indices) and
+                   np.array_equal(gsub_x, ref4.values))
+    by4 = 2 * (12 * nnz4 + 8 * (n4 + 1)) + 4 * nnz4 + 8 * (n4 + 1) + 12 * nnzc + 8 * (n4 + 1)
+    out["config4_masked_spgemm_min_plus_int64"] = {
+        "workload": "C<A.S> = A min.plus A (GrB_mxm, GrB_DESC_S), R-MAT s20, INT64 weights in [1,255]",
+        "nnz_A": nnz4, "nnz_C": nnzc, "ms": t4 * 1e3, "gteps": work / t4 / 1e9,
+        "gteps_def": "sum over mask entries (i,j) of deg_out(i) + deg_in(j), per second",
+        "alg_bytes": by4, "hbm_GBs": by4 / t4 / 1e9, "parity_vs_oracle_256_rows": parity4}
+    for h in (B, C):
+        lib.GrB_Matrix_free(ctypes.byref(h))
+    return out
 
 
 def main():
@@ -314,6 +443,10 @@ def main():
         copy_gbs = 5 * 2 * xs.numel() / (time.perf_counter() - c0) / 1e9
         del xs, ys
 
+    secondary = None
+    if rank == 0 and world == 1 and not args.no_secondary:
+        secondary = secondary_workloads(lib, torch, stream, O, args)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         G = O.Csr(n, n, "BOOL", ap, ai, np.ones(ai.size, np.bool_))
@@ -362,6 +495,7 @@ def main():
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,
             "ingest_s": ingest_s,
+            "secondary": secondary,
         }
         print(json.dumps(out), flush=True)
     if dist:
