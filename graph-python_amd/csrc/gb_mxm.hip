@@ -93,6 +93,115 @@ __global__ __launch_bounds__(MXM_BLOCK) void k_dot_masked(
     }
 }
 
+// Masked dot with G lanes per mask entry, for monoids that are exactly
+// associative and commutative on Z (MIN/MAX/logical/bitwise, integer
+// PLUS/TIMES): the lanes split the shorter of the two lists and binary-search
+// each k in the longer one (independent loads, no serial merge), then fold
+// their partials across the group.
+template <class SR, class X, class Z, int G>
+__global__ __launch_bounds__(MXM_BLOCK) void k_dot_masked_group(
+    SR sr, int64_t nm, const int64_t *__restrict__ mrowof, const int32_t *__restrict__ mci,
+    const int64_t *__restrict__ arp, const int32_t *__restrict__ aci, const X *__restrict__ avx, bool a_iso,
+    const int64_t *__restrict__ brp, const int32_t *__restrict__ bci, const X *__restrict__ bvx, bool b_iso,
+    Z *__restrict__ tval, int64_t *__restrict__ tflag) {
+    const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int gl = (int)(tid & (G - 1));
+    const int64_t ngroups = ((int64_t)gridDim.x * blockDim.x) / G;
+    for (int64_t q = tid / G; q < nm; q += ngroups) {
+        const int64_t i = mrowof[q];
+        const int32_t j = mci[q];
+        const int64_t pa0 = arp[i], ea = arp[i + 1], pb0 = brp[j], eb = brp[j + 1];
+        const bool a_short = (ea - pa0) <= (eb - pb0);
+        const int32_t *__restrict__ sci = a_short ? aci : bci;
+        const int32_t *__restrict__ lci = a_short ? bci : aci;
+        const int64_t ps0 = a_short ? pa0 : pb0, es = a_short ? ea : eb;
+        const int64_t pl0 = a_short ? pb0 : pa0, el = a_short ? eb : ea;
+        bool found = false;
+        Z acc = Z();
+        const int64_t L = el - pl0;
+        if (G == 64 && L >= 256) {
+            // a wave per entry: 64 evenly spaced samples of the long list (one load per
+            // lane) narrow every search to one 1/64 bucket by shuffles, before any
+            // dependent global load
+            const int32_t samp = lci[pl0 + (((int64_t)gl * L) >> 6)];
+            for (int64_t base = 0; base < es - ps0; base += 64) {
+                const int64_t ps = ps0 + base + gl;
+                const bool act = ps < es;
+                const int32_t k = act ? sci[ps] : 0x7fffffff;
+                int bk = 0;
+#pragma unroll
+                for (int st = 32; st > 0; st >>= 1)
+                    if (__shfl(samp, bk + st, 64) <= k) bk += st;
+                if (!act) continue;
+                int64_t a = pl0 + (((int64_t)bk * L) >> 6);
+                int64_t b = bk == 63 ? el : pl0 + (((int64_t)(bk + 1) * L) >> 6) + 1;
+                if (b > el) b = el;
+                while (a < b) {
+                    const int64_t mid = (a + b) >> 1;
+                    if (lci[mid] < k) a = mid + 1;
+                    else b = mid;
+                }
+                if (a < el && lci[a] == k) {
+                    const int64_t pa = a_short ? ps : a, pb = a_short ? a : ps;
+                    X av = X(), bv = X();
+                    if (SR::reads_values && avx && bvx) {
+                        av = avx[a_iso ? 0 : pa];
+                        bv = bvx[b_iso ? 0 : pb];
+                    }
+                    const Z z = sr.mult(av, bv, i, k, j);
+                    acc = found ? sr.add(acc, z) : z;
+                    found = true;
+                }
+            }
+        }
+        int64_t lo = pl0;  // this lane's k values increase: the search window only shrinks
+        for (int64_t ps = ps0 + gl; !(G == 64 && L >= 256) && ps < es && lo < el; ps += G) {
+            const int32_t k = sci[ps];
+            int64_t a = lo, b = el;  // first position with lci >= k
+            while (a < b) {
+                const int64_t mid = (a + b) >> 1;
+                if (lci[mid] < k) a = mid + 1;
+                else b = mid;
+            }
+            lo = a;
+            if (a < el && lci[a] == k) {
+                const int64_t pa = a_short ? ps : a, pb = a_short ? a : ps;
+                X av = X(), bv = X();
+                if (SR::reads_values && avx && bvx) {
+                    av = avx[a_iso ? 0 : pa];
+                    bv = bvx[b_iso ? 0 : pb];
+                }
+                const Z z = sr.mult(av, bv, i, k, j);
+                acc = found ? sr.add(acc, z) : z;
+                found = true;
+            }
+        }
+#pragma unroll
+        for (int off = G >> 1; off > 0; off >>= 1) {
+            const bool of = __shfl_xor((int)found, off, G);
+            const Z oz = gb_shfl_xor(acc, off, G);
+            if (of) {
+                acc = found ? sr.add(acc, oz) : oz;
+                found = true;
+            }
+        }
+        if (gl == 0) {
+            tflag[q] = found ? 1 : 0;
+            if (found) tval[q] = acc;
+        }
+    }
+}
+
+static bool exact_monoid(int mon, int zcode) {
+    switch (mon) {
+    case GBAMD_MON_MIN: case GBAMD_MON_MAX: case GBAMD_MON_LOR: case GBAMD_MON_LAND: case GBAMD_MON_LXOR:
+    case GBAMD_MON_LXNOR: case GBAMD_MON_BOR: case GBAMD_MON_BAND: case GBAMD_MON_BXOR: case GBAMD_MON_BXNOR:
+        return true;
+    case GBAMD_MON_PLUS: case GBAMD_MON_TIMES: return zcode != GBAMD_T_FP32 && zcode != GBAMD_T_FP64;
+    default: return false;  // ANY keeps the first k: the sequential merge does that
+    }
+}
+
 __global__ void k_gather_rowptr(const int64_t *__restrict__ mrp, const int64_t *__restrict__ pos, int64_t nrows,
                                 int64_t *__restrict__ trp) {
     MXM_STRIDE(i, nrows + 1) trp[i] = pos[mrp[i]];
@@ -233,10 +342,25 @@ void gb_spgemm(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, gb_csr_view *BT
             using SRT = decltype(srf);
             using X = decltype(x);
             using Z = decltype(z);
-            if (nm)
+            int64_t gsel = gb_knob("dot_group");  // 0 auto (a wave per entry), 1 thread per entry, else lanes
+            if (gsel == 0) gsel = 64;
+            if (nm && gsel > 1 && exact_monoid(info.mon, info.zcode)) {
+                const unsigned g = mxm_grid(std::min<int64_t>(nm * gsel, 1LL << 24));
+#define GB_DOT_GROUP(GG)                                                                                 \
+    hipLaunchKernelGGL((k_dot_masked_group<SRT, X, Z, GG>), dim3(g), dim3(MXM_BLOCK), 0, gb_stream(), srf, nm, \
+                       mrowof, mask.colidx, A.rowptr, A.colidx, (const X *)av, A.iso, BT->rowptr, BT->colidx, \
+                       (const X *)btv, BT->iso, (Z *)tval, flag)
+                if (gsel <= 4) GB_DOT_GROUP(4);
+                else if (gsel <= 8) GB_DOT_GROUP(8);
+                else if (gsel <= 16) GB_DOT_GROUP(16);
+                else if (gsel <= 32) GB_DOT_GROUP(32);
+                else GB_DOT_GROUP(64);
+#undef GB_DOT_GROUP
+            } else if (nm) {
                 hipLaunchKernelGGL((k_dot_masked<SRT, X, Z>), dim3(mxm_grid(nm)), dim3(MXM_BLOCK), 0, gb_stream(),
                                    srf, nm, mrowof, mask.colidx, A.rowptr, A.colidx, (const X *)av, A.iso,
                                    BT->rowptr, BT->colidx, (const X *)btv, BT->iso, (Z *)tval, flag);
+            }
             GB_LAUNCH_CHECK();
             gb_exclusive_scan_i64(flag, pos, nm);
             int64_t nz = gb_read_i64(pos + nm);

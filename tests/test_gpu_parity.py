@@ -428,6 +428,7 @@ def _skewed_csr(rng, n, dtype):
     lens = rng.integers(0, 12, n)
     lens[::17] = rng.integers(129, 3000, lens[::17].size)
     lens[5] = n  # a full row
+    lens = np.minimum(lens, n)
     r = np.repeat(np.arange(n), lens)
     c = np.concatenate([rng.choice(n, size=min(L, n), replace=False) for L in lens])
     if dtype in ("FP32", "FP64"):
@@ -472,6 +473,35 @@ def test_spmv_long_rows_vs_oracle(gb, name, mon, mul, dt, udense):
                                        atol=1e-3 if dt == "FP32" else 1e-10)
         else:
             assert np.array_equal(gv, ref.values)
+
+
+@pytest.mark.parametrize("name,mon,mul,dt", [("min_plus", "MIN", "PLUS", "INT64"),
+                                             ("plus_times", "PLUS", "TIMES", "INT64"),
+                                             ("max_second", "MAX", "SECOND", "INT16"),
+                                             ("plus_times", "PLUS", "TIMES", "FP64"),
+                                             ("min_secondi", "MIN", "SECONDI", "INT64"),
+                                             ("any_pair", "ANY", "PAIR", "INT64")])
+@pytest.mark.parametrize("group", [0, 1, 8])  # dot kernel: auto (wave per entry), thread per entry, 8 lanes
+def test_masked_spgemm_long_lists_vs_oracle(gb, name, mon, mul, dt, group):
+    """C<A.S> = A (+).(x) A on a matrix with rows up to 3000 entries: the masked dot's
+    sampled-bucket search (lists >= 256) and the galloping merge both run."""
+    rng = np.random.default_rng(hash((name, dt, "spgemm-long")) % 2**32)
+    n = 2000
+    Ao = _skewed_csr(rng, n, dt)
+    Ag = _to_gb(gb, Ao)
+    sr = getattr(gb.semiring, name)[dt]
+    gb.set_knob("dot_group", group)
+    try:
+        Cg = Ag.mxm(Ag, sr).new(mask=Ag.S)
+    finally:
+        gb.set_knob("dot_group", 0)
+    ref = O.mxm(O.Csr.empty(n, n, dt), Ao, Ao, (mon, mul, dt), mask=Ao, mask_struct=True)
+    if mon == "ANY":
+        r, c, _ = Cg.to_coo()
+        er, ec, _ = ref.to_coo()
+        assert np.array_equal(r.astype(np.int64), er) and np.array_equal(c.astype(np.int64), ec)
+    else:
+        _check_mat(Cg, ref, fp=dt in ("FP32", "FP64"))
 
 
 @pytest.mark.parametrize("scale", [10, 12, 14])

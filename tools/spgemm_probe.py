@@ -36,20 +36,28 @@ dout = np.diff(ap)
 din = np.bincount(ai, minlength=n)
 rows = np.repeat(np.arange(n), dout)
 work = int((dout[rows] + din[ai]).sum())
-C = ctypes.c_void_p()
-lib.GrB_Matrix_new(ctypes.byref(C), lib.GrB_INT64, n, n)
 sr = lib.GrB_MIN_PLUS_SEMIRING_INT64
-for method in sys.argv[3:] or ["0"]:
-    gb.set_knob("mxm_method", int(method))
+
+
+def run():
+    C = ctypes.c_void_p()  # C = A.mxm(A).new(mask=A.S): a fresh output each call
+    lib.GrB_Matrix_new(ctypes.byref(C), lib.GrB_INT64, n, n)
     lib.GrB_mxm(C, A, None, sr, A, A, lib.GrB_DESC_S)
+    lib.GrB_Matrix_nvals(ctypes.byref(nv), C)
+    lib.GrB_Matrix_free(ctypes.byref(C))
+    return nv.value
+
+
+for g in sys.argv[3:] or ["0"]:
+    gb.set_knob("dot_group", int(g))
+    run()
     torch.cuda.synchronize()
     ts = []
     for _ in range(reps):
         t0 = time.perf_counter()
-        lib.GrB_mxm(C, A, None, sr, A, A, lib.GrB_DESC_S)
-        lib.GrB_Matrix_nvals(ctypes.byref(nv), C)
+        nc = run()
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
     t = min(ts)
-    print(f"s{scale} method {method}: nnz(A) {nnz} nnz(C) {nv.value} work {work:.3e} time {t*1e3:.2f} ms "
+    print(f"s{scale} dot_group {g}: nnz(A) {nnz} nnz(C) {nc} work {work:.3e} time {t*1e3:.2f} ms "
           f"GTEPS {work / t / 1e9:.2f}", flush=True)
