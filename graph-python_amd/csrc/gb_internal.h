@@ -241,6 +241,7 @@ struct gb_bitmap_view {
     const void *vals = nullptr;
     bool iso = false;
     int tcode = 0;
+    const int64_t *count = nullptr;      // device count of entries (nullptr: unknown)
     const long long *mf_hint = nullptr;  // device edge count of the entries (see GB_Obj::hint_key)
     const void *hint_key = nullptr;
     gb_scratch own;

@@ -648,7 +648,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
     const X *__restrict__ uvals, bool u_iso, const uint64_t *__restrict__ mbits, bool mcomp,
     const int32_t *__restrict__ chunks, int64_t nchunks, Z *__restrict__ cpart, int8_t *__restrict__ cfound,
     uint64_t *__restrict__ tbits, Z *__restrict__ tvals, unsigned long long *__restrict__ tcount,
-    unsigned long long *__restrict__ gst) {
+    unsigned long long *__restrict__ gst, const int64_t *__restrict__ ucount, int64_t un) {
     __shared__ Z accs[WAVES_PER_BLOCK][64];
     __shared__ int fls[WAVES_PER_BLOCK][64];
     Z *acc = accs[threadIdx.x >> 6];
@@ -663,6 +663,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
         if (a_iso) a0 = avals[0];
         if (u_iso) u0 = uvals[0];
     }
+    const bool ufull = ucount && *ucount == un;  // u has every entry: no presence tests
     fl[lane] = 0;
     gb_wave_sync();
     long long cnt = 0;
@@ -685,7 +686,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
                 }
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
-                    if (!ok[u] || !gb_bit(ubits, kk[u])) continue;
+                    if (!ok[u] || (!ufull && !gb_bit(ubits, kk[u]))) continue;
                     Z t;
                     gb_spmv_product<SR, X, Z, FLIP>(sr, rv, avals, a_iso, a0, uvals, u_iso, u0, q + 64 * u, kk[u],
                                                     r, t);
@@ -744,7 +745,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
             }
 #pragma unroll
             for (int u = 0; u < 4; u++) {
-                bool f = ok[u] && gb_bit(ubits, k[u]);
+                bool f = ok[u] && (ufull || gb_bit(ubits, k[u]));
                 Z z = Z();
                 if (f)
                     gb_spmv_product<SR, X, Z, FLIP>(sr, rv, avals, a_iso, a0, uvals, u_iso, u0, pos[u], k[u],
@@ -1104,17 +1105,18 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             Z *cpart = s.get<Z>(A.nlchunks + 1);
             int8_t *cfound = s.get<int8_t>(A.nlchunks + 1);
             const int64_t units = std::max<int64_t>(nw, A.nlchunks);
+            const bool u_iso_k = u.iso || gb_knob("spmv_timing_no_x_gather") == 1;  // timing experiment only
             const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 3) / 4, 4096));
             if (flip)
                 hipLaunchKernelGGL((k_spmv_words<SRT, X, Z, true>), dim3(grid), dim3(SPMV_BLOCK), 0, gb_stream(), srf,
-                                   n, A.rowptr, A.colidx, (const X *)av, A.iso, u.bits, (const X *)uv, u.iso,
+                                   n, A.rowptr, A.colidx, (const X *)av, A.iso, u.bits, (const X *)uv, u_iso_k,
                                    mask.bits, mask.comp, A.lchunks, A.nlchunks, cpart, cfound, T.bits, (Z *)T.dense,
-                                   (unsigned long long *)T.d_nvals, gst);
+                                   (unsigned long long *)T.d_nvals, gst, u.count, u.n);
             else
                 hipLaunchKernelGGL((k_spmv_words<SRT, X, Z, false>), dim3(grid), dim3(SPMV_BLOCK), 0, gb_stream(),
-                                   srf, n, A.rowptr, A.colidx, (const X *)av, A.iso, u.bits, (const X *)uv, u.iso,
+                                   srf, n, A.rowptr, A.colidx, (const X *)av, A.iso, u.bits, (const X *)uv, u_iso_k,
                                    mask.bits, mask.comp, A.lchunks, A.nlchunks, cpart, cfound, T.bits, (Z *)T.dense,
-                                   (unsigned long long *)T.d_nvals, gst);
+                                   (unsigned long long *)T.d_nvals, gst, u.count, u.n);
             GB_LAUNCH_CHECK();
             if (A.nlchunks > 0) {
                 const unsigned fg = (unsigned)std::max<int64_t>(1, std::min<int64_t>((A.nlchunks + 255) / 256, 1024));

@@ -314,6 +314,7 @@ void gb_get_bitmap(gb_bitmap_view &v, GB_Obj *A) {
         v.n = A->nrows;
         v.bits = A->bits;
         v.iso = A->iso;
+        v.count = A->d_nvals;
         if (!A->dense) {  // empty vector: give kernels a valid value pointer
             void *d = v.own.get<char>(A->type->size);
             gb_memset(d, 0, A->type->size);
@@ -334,6 +335,7 @@ void gb_get_bitmap(gb_bitmap_view &v, GB_Obj *A) {
     v.own.ptrs[v.own.n++] = bits;
     v.own.ptrs[v.own.n++] = dense;
     v.own.ptrs[v.own.n++] = cnt;
+    v.count = cnt;
     v.n = A->nrows;
     v.bits = bits;
     v.vals = dense;

@@ -17,6 +17,8 @@ ef = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 lib = gb.lib
 stream = torch.cuda.Stream()
 gb.set_stream(stream)
+if os.environ.get("SPMV_NO_X_GATHER"):  # timing experiment: x treated as iso (wrong values)
+    gb.set_knob("spmv_timing_no_x_gather", 1)
 n = 1 << scale
 A = ctypes.c_void_p()
 assert lib.GxB_Matrix_rmat(ctypes.byref(A), scale, ef, 42, 2, 2, 0, 0) == 0
