@@ -641,6 +641,173 @@ __device__ __forceinline__ void gb_spmv_product(SR &sr, bool rv, const X *__rest
     z = FLIP ? sr.mult(b, a, 0, k, r) : sr.mult(a, b, r, k, 0);
 }
 
+// Merge-path word (general SpMV, mode 1): the word's concatenated entries are
+// cut into 64 equal contiguous runs, one per lane; a lane folds its run
+// sequentially (row changes read from LDS, four entries' loads issued ahead),
+// rows wholly inside one run are finished by that lane, and rows crossing runs
+// are folded by their owner lane from the runs' carries in lane order.
+template <class Z>
+struct gb_mp_lds {
+    int incl[64];
+    int64_t p0[64];
+    Z pa[64], pb[64];  // carry of the row continuing from the previous run / into the next
+    int fa[64], fb[64];
+};
+
+template <class SR, class X, class Z, bool FLIP>
+__device__ __forceinline__ long long gb_spmv_words_mp(
+    SR &sr, int64_t nrows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ colidx,
+    const X *__restrict__ avals, bool a_iso, X a0, const uint64_t *__restrict__ ubits, const X *__restrict__ uvals,
+    bool u_iso, X u0, const uint64_t *__restrict__ mbits, bool mcomp, bool ufull, bool rv,
+    uint64_t *__restrict__ tbits, Z *__restrict__ tvals, Z *acc, int *fl, gb_mp_lds<Z> &M) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const int64_t nwords = (nrows + 63) >> 6;
+    long long cnt = 0;
+    for (int64_t w = wave; w < nwords; w += nwaves) {
+        const int64_t r = (w << 6) + lane;
+        bool open = r < nrows;
+        if (open && mbits) open = gb_bit(mbits, r) != mcomp;
+        int64_t p0 = 0;
+        int len = 0;
+        if (open) {
+            p0 = rowptr[r];
+            const int64_t d = rowptr[r + 1] - p0;
+            len = d > SPMV_LONG ? 0 : (int)d;  // long rows: chunks + k_spmv_fold
+        }
+        int incl = len;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += y;
+        }
+        const int total = __shfl(incl, 63, 64);
+        M.incl[lane] = incl;
+        M.p0[lane] = p0;
+        M.fa[lane] = 0;
+        M.fb[lane] = 0;
+        gb_wave_sync();
+        if (total > 0) {
+            const int c = (total + 63) >> 6;
+            const int s0 = lane * c;
+            const int e1 = s0 + c < total ? s0 + c : total;
+            if (s0 < e1) {
+                int row = 0;  // first row with incl > s0
+#pragma unroll
+                for (int st = 32; st > 0; st >>= 1)
+                    if (M.incl[row + st - 1] <= s0) row += st;
+                int rbeg = row ? M.incl[row - 1] : 0, rend = M.incl[row];
+                bool before = rbeg < s0;
+                int64_t pbase = M.p0[row] - rbeg;
+                bool f = false;
+                Z z = Z();
+                for (int e = s0; e < e1; e += 4) {
+                    int rw[4];
+                    int64_t pos[4];
+                    bool ok[4];
+                    // positions of the next four entries (row changes from LDS)
+                    int trow = row, tbeg = rbeg, tend = rend;
+                    int64_t tbase = pbase;
+#pragma unroll
+                    for (int t = 0; t < 4; t++) {
+                        const int et = e + t;
+                        ok[t] = et < e1;
+                        if (ok[t]) {
+                            while (et >= tend) {
+                                trow++;
+                                tbeg = tend;
+                                tend = M.incl[trow];
+                                tbase = M.p0[trow] - tbeg;
+                            }
+                        }
+                        rw[t] = trow;
+                        pos[t] = tbase + et;
+                    }
+                    int k[4];
+#pragma unroll
+                    for (int t = 0; t < 4; t++) k[t] = ok[t] ? colidx[pos[t]] : 0;
+                    bool hit[4];
+                    Z zt[4];
+#pragma unroll
+                    for (int t = 0; t < 4; t++) {
+                        hit[t] = ok[t] && (ufull || gb_bit(ubits, k[t]));
+                        zt[t] = Z();
+                        if (hit[t])
+                            gb_spmv_product<SR, X, Z, FLIP>(sr, rv, avals, a_iso, a0, uvals, u_iso, u0, pos[t], k[t],
+                                                            (w << 6) + rw[t], zt[t]);
+                    }
+#pragma unroll
+                    for (int t = 0; t < 4; t++) {
+                        if (!ok[t]) break;
+                        if (rw[t] != row) {  // the current row closed inside this run
+                            if (before) {
+                                M.pa[lane] = z;
+                                M.fa[lane] = f;
+                            } else if (f) {
+                                acc[row] = z;
+                                fl[row] = 1;
+                            }
+                            row = rw[t];
+                            before = false;
+                            f = false;
+                        }
+                        if (hit[t]) {
+                            z = f ? sr.add(z, zt[t]) : zt[t];
+                            f = true;
+                        }
+                    }
+                    row = trow;
+                    rbeg = tbeg;
+                    rend = tend;
+                    pbase = tbase;
+                }
+                // the row open at the end of the run
+                const bool cont = rend > e1;
+                if (before) {
+                    M.pa[lane] = z;
+                    M.fa[lane] = f;
+                } else if (cont) {
+                    M.pb[lane] = z;
+                    M.fb[lane] = f;
+                } else if (f) {
+                    acc[row] = z;
+                    fl[row] = 1;
+                }
+            }
+            gb_wave_sync();
+            // rows crossing runs: the owner lane folds the carries in lane order
+            if (len > 0) {
+                const int ex = incl - len;
+                const int k0 = ex / c, k1 = (incl - 1) / c;
+                if (k1 > k0) {
+                    bool f = M.fb[k0] != 0;
+                    Z z = M.pb[k0];
+                    for (int k = k0 + 1; k <= k1; k++) {
+                        if (!M.fa[k]) continue;
+                        z = f ? sr.add(z, M.pa[k]) : M.pa[k];
+                        f = true;
+                    }
+                    if (f) {
+                        acc[lane] = z;
+                        fl[lane] = 1;
+                    }
+                }
+            }
+            gb_wave_sync();
+        }
+        const bool hitrow = fl[lane] != 0;
+        const unsigned long long fmask = __ballot(hitrow);
+        if (hitrow) tvals[r] = acc[lane];
+        if (lane == 0) {
+            tbits[w] = fmask;
+            cnt += __popcll(fmask);
+        }
+        fl[lane] = 0;
+        gb_wave_sync();
+    }
+    return cnt;
+}
+
 template <class SR, class X, class Z, bool FLIP>
 __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
     SR sr, int64_t nrows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ colidx,
@@ -648,9 +815,10 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
     const X *__restrict__ uvals, bool u_iso, const uint64_t *__restrict__ mbits, bool mcomp,
     const int32_t *__restrict__ chunks, int64_t nchunks, Z *__restrict__ cpart, int8_t *__restrict__ cfound,
     uint64_t *__restrict__ tbits, Z *__restrict__ tvals, unsigned long long *__restrict__ tcount,
-    unsigned long long *__restrict__ gst, const int64_t *__restrict__ ucount, int64_t un) {
+    unsigned long long *__restrict__ gst, const int64_t *__restrict__ ucount, int64_t un, int mode) {
     __shared__ Z accs[WAVES_PER_BLOCK][64];
     __shared__ int fls[WAVES_PER_BLOCK][64];
+    __shared__ gb_mp_lds<Z> mps[WAVES_PER_BLOCK];
     Z *acc = accs[threadIdx.x >> 6];
     int *fl = fls[threadIdx.x >> 6];  // row has at least one product
     const int lane = threadIdx.x & 63;
@@ -709,6 +877,13 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
         }
     }
     // output words
+    if (mode == 1) {
+        cnt += gb_spmv_words_mp<SR, X, Z, FLIP>(sr, nrows, rowptr, colidx, avals, a_iso, a0, ubits, uvals, u_iso, u0,
+                                                mbits, mcomp, ufull, rv, tbits, tvals, acc, fl, mps[threadIdx.x >> 6]);
+        long long tot;
+        if (gb_grid_sum(cnt, gst, &tot)) *tcount = (unsigned long long)tot;
+        return;
+    }
     for (int64_t w = wave; w < nwords; w += nwaves) {
         const int64_t r = (w << 6) + lane;
         bool open = r < nrows;
@@ -1106,17 +1281,18 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             int8_t *cfound = s.get<int8_t>(A.nlchunks + 1);
             const int64_t units = std::max<int64_t>(nw, A.nlchunks);
             const bool u_iso_k = u.iso || gb_knob("spmv_timing_no_x_gather") == 1;  // timing experiment only
+            const int spmv_mode = gb_knob("spmv_words") == 1 ? 0 : 1;  // 1: merge path (default), 0: segmented scan
             const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 3) / 4, 4096));
             if (flip)
                 hipLaunchKernelGGL((k_spmv_words<SRT, X, Z, true>), dim3(grid), dim3(SPMV_BLOCK), 0, gb_stream(), srf,
                                    n, A.rowptr, A.colidx, (const X *)av, A.iso, u.bits, (const X *)uv, u_iso_k,
                                    mask.bits, mask.comp, A.lchunks, A.nlchunks, cpart, cfound, T.bits, (Z *)T.dense,
-                                   (unsigned long long *)T.d_nvals, gst, u.count, u.n);
+                                   (unsigned long long *)T.d_nvals, gst, u.count, u.n, spmv_mode);
             else
                 hipLaunchKernelGGL((k_spmv_words<SRT, X, Z, false>), dim3(grid), dim3(SPMV_BLOCK), 0, gb_stream(),
                                    srf, n, A.rowptr, A.colidx, (const X *)av, A.iso, u.bits, (const X *)uv, u_iso_k,
                                    mask.bits, mask.comp, A.lchunks, A.nlchunks, cpart, cfound, T.bits, (Z *)T.dense,
-                                   (unsigned long long *)T.d_nvals, gst, u.count, u.n);
+                                   (unsigned long long *)T.d_nvals, gst, u.count, u.n, spmv_mode);
             GB_LAUNCH_CHECK();
             if (A.nlchunks > 0) {
                 const unsigned fg = (unsigned)std::max<int64_t>(1, std::min<int64_t>((A.nlchunks + 255) / 256, 1024));

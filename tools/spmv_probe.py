@@ -19,6 +19,8 @@ stream = torch.cuda.Stream()
 gb.set_stream(stream)
 if os.environ.get("SPMV_NO_X_GATHER"):  # timing experiment: x treated as iso (wrong values)
     gb.set_knob("spmv_timing_no_x_gather", 1)
+if os.environ.get("SPMV_WORDS"):  # 1: segmented-scan words kernel instead of merge path
+    gb.set_knob("spmv_words", int(os.environ["SPMV_WORDS"]))
 n = 1 << scale
 A = ctypes.c_void_p()
 assert lib.GxB_Matrix_rmat(ctypes.byref(A), scale, ef, 42, 2, 2, 0, 0) == 0
