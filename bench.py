@@ -295,14 +295,33 @@ def main():
     nv = ctypes.c_uint64()
     ev_pairs, level_counts = [], []
 
+    zero_copy = world > 1 and part["slot"] * world == words
+
+    def exchange_frontier(into_q_bits):
+        """all-gather the ranks' frontier slices (RCCL, on the library stream) into q"""
+        ok(lib.GxB_Vector_bitmap_export(qloc, ctypes.c_void_p(exchange.send.data_ptr()), hi_w - lo_w), "bm out")
+        with torch.cuda.stream(stream):
+            gath = exchange.run(into_q_bits)  # into_q_bits: straight into q's device bitmap
+        if into_q_bits is not None:
+            ok(lib.GxB_Vector_device_touch(q), "touch q")
+        else:
+            ok(lib.GxB_Vector_bitmap_import(q, ctypes.c_void_p(gath.data_ptr()), words), "bm in")
+
     def bfs(src, timing):
         ok(lib.GrB_Vector_clear(q), "clear q")
         ok(lib.GrB_Vector_clear(v), "clear v")
-        ok(lib.GrB_Vector_setElement_BOOL(q, True, int(src)), "q[src]")
-        if world > 1:
+        q_bits = None
+        if world == 1:
+            ok(lib.GrB_Vector_setElement_BOOL(q, True, int(src)), "q[src]")
+        else:
             ok(lib.GrB_Vector_clear(qloc), "clear qloc")
             if lo <= src < hi:
                 ok(lib.GrB_Vector_setElement_BOOL(qloc, True, int(src) - lo), "qloc[src]")
+            exchange_frontier(None)  # q = root, iso true
+            if zero_copy:
+                from graphblas_amd import device as gdev
+
+                q_bits = gdev.device_tensor(torch, gdev.vector_view(q).bitmap, words)
         d = 0
         while True:
             d += 1
@@ -332,11 +351,7 @@ def main():
                     e1.record(stream)
                     ev_pairs.append((e0, e1))
                 # exchange: all-gather the frontier bitmap over RCCL (stream-ordered)
-                ok(lib.GxB_Vector_bitmap_export(qloc, ctypes.c_void_p(exchange.send.data_ptr()), hi_w - lo_w),
-                   "bm out")
-                with torch.cuda.stream(stream):
-                    gath = exchange.run()
-                ok(lib.GxB_Vector_bitmap_import(q, ctypes.c_void_p(gath.data_ptr()), words), "bm in")
+                exchange_frontier(q_bits)
             ok(lib.GrB_Vector_nvals(ctypes.byref(nv), q), "nvals")
             if nv.value == 0:
                 break

@@ -1281,7 +1281,7 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             int8_t *cfound = s.get<int8_t>(A.nlchunks + 1);
             const int64_t units = std::max<int64_t>(nw, A.nlchunks);
             const bool u_iso_k = u.iso || gb_knob("spmv_timing_no_x_gather") == 1;  // timing experiment only
-            const int spmv_mode = gb_knob("spmv_words") == 1 ? 0 : 1;  // 1: merge path (default), 0: segmented scan
+            const int spmv_mode = gb_knob("spmv_words") == 2 ? 1 : 0;  // 0: segmented scan (default), 2: merge path
             const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 3) / 4, 4096));
             if (flip)
                 hipLaunchKernelGGL((k_spmv_words<SRT, X, Z, true>), dim3(grid), dim3(SPMV_BLOCK), 0, gb_stream(), srf,

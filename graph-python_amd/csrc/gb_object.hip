@@ -1360,13 +1360,22 @@ GrB_Info GxB_Matrix_device_view(GxB_DeviceView *view, const GrB_Matrix A) {
 GrB_Info GxB_Vector_device_view(GxB_DeviceView *view, const GrB_Vector v) {
     return GxB_Matrix_device_view(view, (GrB_Matrix)v);
 }
+// recount a vector whose bitmap was rewritten on the device; the count is
+// published to the host mailbox, so a following nvals spins instead of copying
+static void vec_recount_published(GB_Obj *o) {
+    if (!o->pub) o->pub = gb_host_slot_alloc();
+    const uint64_t seq = gb_next_pub_seq();
+    gb_bitmap_count_pub(o->bits, o->nrows, o->d_nvals, o->pub, seq);
+    o->nvals_valid = false;
+    o->hint_valid = false;
+    o->pub_seq = seq;
+    o->pub_epoch = gb_epoch();
+}
 GrB_Info GxB_Vector_device_touch(GrB_Vector v) {
     return gb_api(OBJ(v), [&] {
         GB_Obj *o = gb_obj_check(v);
         GB_REQUIRE(o->kind != GB_KIND_MATRIX, GrB_INVALID_OBJECT, "not a vector");
-        gb_bitmap_count(o->bits, o->nrows, o->d_nvals);
-        o->nvals_valid = false;
-        o->hint_valid = false;
+        vec_recount_published(o);
     });
 }
 GrB_Info GxB_Vector_bitmap_export(GrB_Vector v, void *dst, GrB_Index nwords) {
@@ -1397,9 +1406,7 @@ GrB_Info GxB_Vector_bitmap_import(GrB_Vector v, const void *src, GrB_Index nword
         }
         gb_copy_h2d(o->dense, one, ts);
         o->iso = true;
-        gb_bitmap_count(o->bits, o->nrows, o->d_nvals);
-        o->nvals_valid = false;
-        o->hint_valid = false;
+        vec_recount_published(o);
     });
 }
 GrB_Info GxB_Matrix_prepare_transpose(GrB_Matrix A) {

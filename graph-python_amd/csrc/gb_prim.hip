@@ -168,15 +168,36 @@ __global__ void k_bitmap_count(const uint64_t *__restrict__ bits, int64_t nwords
     if (threadIdx.x == 0 && part) atomicAdd(count, part);
 }
 
-void gb_bitmap_count(const uint64_t *bits, int64_t n, int64_t *d_count) {
-    gb_memset(d_count, 0, sizeof(int64_t));
-    int64_t nw = gb_words(n);
-    if (nw == 0) return;
+// one launch: grid-wide popcount, the finishing block stores the count (no prior
+// zeroing) and, when given a host mailbox, publishes it there too
+__global__ void k_bitmap_count_store(const uint64_t *__restrict__ bits, int64_t nwords, int64_t *__restrict__ count,
+                                     unsigned long long *__restrict__ gst, gb_host_slot *pub, long long seq) {
+    long long c = 0;
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nwords;
+         w += (int64_t)gridDim.x * blockDim.x)
+        c += __popcll(bits[w]);
+    long long tot;
+    if (gb_grid_sum(c, gst, &tot)) {
+        *count = tot;
+        if (pub) {
+            __hip_atomic_store(&pub->value, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __threadfence_system();
+            __hip_atomic_store(&pub->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+void gb_bitmap_count_pub(const uint64_t *bits, int64_t n, int64_t *d_count, gb_host_slot *pub_host, uint64_t seq) {
+    const int64_t nw = gb_words(n);
     unsigned g = gb_grid(nw);
-    if (g > 1024) g = 1024;
-    hipLaunchKernelGGL(k_bitmap_count, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), bits, nw,
-                       (unsigned long long *)d_count);
+    if (g > 512) g = 512;
+    hipLaunchKernelGGL(k_bitmap_count_store, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), bits, nw, d_count,
+                       gb_device_state(), pub_host ? gb_host_slot_device(pub_host) : nullptr, (long long)seq);
     GB_LAUNCH_CHECK();
+}
+
+void gb_bitmap_count(const uint64_t *bits, int64_t n, int64_t *d_count) {
+    gb_bitmap_count_pub(bits, n, d_count, nullptr, 0);
 }
 
 // per-word popcount -> exclusive scan -> positions

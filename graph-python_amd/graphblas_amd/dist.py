@@ -37,16 +37,25 @@ class BitmapAllGather:
         self.gathered = torch.zeros(part["slot"] * world, dtype=torch.int64, device=device)
         self._fused = dist.get_backend() == "nccl"
 
-    def run(self):
+    def run(self, out=None):
+        """Gather into `out` (e.g. a vector's device bitmap, slot*world words) or the
+        internal buffer; returns the tensor gathered into."""
+        out = self.gathered if out is None else out
         if self._fused:
-            self.dist.all_gather_into_tensor(self.gathered, self.send)
+            self.dist.all_gather_into_tensor(out, self.send)
         elif self.send.is_cuda:  # gloo rehearsal of the GPU path: stage through host memory
-            host = self.gathered.cpu()
+            host = torch_empty_like_cpu(out)
             self.dist.all_gather(list(host.chunk(self.world)), self.send.cpu())
-            self.gathered.copy_(host)
+            out.copy_(host)
         else:
-            self.dist.all_gather(list(self.gathered.chunk(self.world)), self.send)
-        return self.gathered
+            self.dist.all_gather(list(out.chunk(self.world)), self.send)
+        return out
+
+
+def torch_empty_like_cpu(t):
+    import torch
+
+    return torch.empty(t.shape, dtype=t.dtype)
 
 
 def pack_bits(mask_bool, nwords):
