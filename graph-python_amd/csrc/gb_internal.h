@@ -167,6 +167,8 @@ uint64_t gb_epoch();
 hipStream_t gb_stream_peek();  // the library stream, without counting an enqueue
 // wait for slot->seq == seq; false if the stream drained without it (caller falls back)
 bool gb_host_slot_wait(gb_host_slot *s, uint64_t seq, int64_t *value);
+// zero nw bitmap words and (if given) the count, in one launch
+void gb_zero_bitmap(uint64_t *bits, int64_t nw, int64_t *d_count);
 // count the set bits into *d_count (one launch); publish to the host mailbox when given
 void gb_bitmap_count_pub(const uint64_t *bits, int64_t n, int64_t *d_count, gb_host_slot *pub_host, uint64_t seq);  // tuning knobs (0 = auto)
 

@@ -62,10 +62,9 @@ static void alloc_empty_storage(GB_Obj *A) {
     } else {
         int64_t nw = gb_words(A->nrows);
         A->bits = gb_malloc_n<uint64_t>(nw);
-        gb_memset(A->bits, 0, nw * sizeof(uint64_t));
         A->dense = nullptr;
         if (!A->d_nvals) A->d_nvals = gb_malloc_n<int64_t>(1);
-        gb_memset(A->d_nvals, 0, sizeof(int64_t));
+        gb_zero_bitmap(A->bits, nw, A->d_nvals);  // one launch: bits and count
         A->nvals = 0;
         A->nvals_valid = true;
         A->hint_valid = false;
@@ -711,10 +710,11 @@ static void matrix_set_element(GB_Obj *A, T x, int64_t i, int64_t j) {
 
 template <class T>
 __global__ void k_vec_set(unsigned long long *__restrict__ bits, T *__restrict__ dense, int64_t i, T x,
-                          unsigned long long *__restrict__ cnt) {
+                          unsigned long long *__restrict__ cnt, T *__restrict__ iso_init) {
     unsigned long long m = 1ULL << (i & 63);
     unsigned long long old = atomicOr(&bits[i >> 6], m);
     if (dense) dense[i] = x;
+    if (iso_init) *iso_init = x;  // first entry of an empty vector: its iso value
     if (!(old & m)) atomicAdd(cnt, 1ULL);
 }
 __global__ void k_vec_clear(unsigned long long *__restrict__ bits, int64_t i, unsigned long long *__restrict__ cnt) {
@@ -726,11 +726,11 @@ __global__ void k_vec_clear(unsigned long long *__restrict__ bits, int64_t i, un
 template <class T>
 static void vector_set_element(GB_Obj *v, T x, int64_t i) {
     GB_REQUIRE(i >= 0 && i < v->nrows, GrB_INVALID_INDEX, "index out of range");
+    T *iso_init = nullptr;
     if (!v->dense) {
-        // first value: store it as an iso vector
+        // first value: store it as an iso vector (the set kernel writes the value)
         v->dense = gb_malloc(sizeof(T));
-        gb_copy_h2d(v->dense, &x, sizeof(T));
-        gb_sync();
+        iso_init = (T *)v->dense;
         v->iso = true;
     } else if (v->iso) {
         T cur;
@@ -745,7 +745,7 @@ static void vector_set_element(GB_Obj *v, T x, int64_t i) {
         }
     }
     hipLaunchKernelGGL(k_vec_set<T>, dim3(1), dim3(1), 0, gb_stream(), (unsigned long long *)v->bits,
-                       v->iso ? nullptr : (T *)v->dense, i, x, (unsigned long long *)v->d_nvals);
+                       v->iso ? nullptr : (T *)v->dense, i, x, (unsigned long long *)v->d_nvals, iso_init);
     GB_LAUNCH_CHECK();
     v->nvals_valid = false;
     v->hint_valid = false;

@@ -467,7 +467,7 @@ __global__ __launch_bounds__(OPS_BLOCK) void k_assign_all_scalar(
     gb_grid_add(delta, count, gst);
 }
 
-// w<M>(:) = x, M a plain (non-complemented) mask, no replace: a wave takes 64
+// w<M>(:) = x, M a plain (non-complemented) mask, no replace: a wave takes 16
 // mask words per step, one per lane (each lane updates its presence word);
 // then the selected values of each non-zero word are written by the whole
 // wave, one lane per position (coalesced stores).
@@ -484,9 +484,9 @@ __global__ __launch_bounds__(OPS_BLOCK) void k_assign_mask_words(int64_t nwords,
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     long long delta = 0;
     if (iso_true) {
-        for (int64_t base = wave * 64; base < nwords; base += nwaves * 64) {
+        for (int64_t base = wave * 16; base < nwords; base += nwaves * 16) {
             const int64_t w = base + lane;
-            const uint64_t m = w < nwords ? mbits[w] : 0;
+            const uint64_t m = (lane < 16 && w < nwords) ? mbits[w] : 0;
             if (m) {
                 const uint64_t c = cbits[w], nwd = c | m;
                 if (nwd != c) cbits[w] = nwd;
@@ -548,7 +548,7 @@ static bool assign_all_scalar_fast(GB_Obj *w, GB_Obj *mask, const char *xc, cons
         memcpy(&xv, xc, sizeof(T));
         if (n && m.bits && !m.comp && !d.replace)
             hipLaunchKernelGGL(k_assign_mask_words<T>,
-                               dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((gb_words(n) + 255) / 256, 1024))),
+                               dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((gb_words(n) + 63) / 64, 2048))),
                                dim3(OPS_BLOCK), 0, gb_stream(), gb_words(n), w->bits, (T *)w->dense, m.bits, m.iso_val,
                                m.iso_code, xv, (unsigned long long *)w->d_nvals, gb_device_state());
         else if (n)

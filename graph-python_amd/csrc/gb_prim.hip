@@ -196,6 +196,19 @@ void gb_bitmap_count_pub(const uint64_t *bits, int64_t n, int64_t *d_count, gb_h
     GB_LAUNCH_CHECK();
 }
 
+__global__ void k_zero_bitmap(uint64_t *__restrict__ bits, int64_t nw, int64_t *__restrict__ count) {
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    for (int64_t w = t; w < nw; w += (int64_t)gridDim.x * blockDim.x) bits[w] = 0;
+    if (t == 0 && count) *count = 0;
+}
+
+void gb_zero_bitmap(uint64_t *bits, int64_t nw, int64_t *d_count) {
+    unsigned g = gb_grid(nw);
+    if (g > 1024) g = 1024;
+    hipLaunchKernelGGL(k_zero_bitmap, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), bits, nw, d_count);
+    GB_LAUNCH_CHECK();
+}
+
 void gb_bitmap_count(const uint64_t *bits, int64_t n, int64_t *d_count) {
     gb_bitmap_count_pub(bits, n, d_count, nullptr, 0);
 }
