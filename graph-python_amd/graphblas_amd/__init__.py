@@ -65,3 +65,4 @@ __all__ = ["Matrix", "Vector", "Scalar", "TransposedMatrix", "Recorder", "binary
            "op", "dtypes", "init", "replace", "backend", "lib"]
 
 from . import dtypes  # noqa: E402
+from . import io  # noqa: E402,F401

@@ -32,6 +32,7 @@ _SIGS = {
     "GxB_Context_set_stream": [P], "GxB_Context_get_stream": [P], "GxB_Context_set_device": [E],
     "GxB_builtin_lookup": [P, P, ctypes.c_char_p], "GxB_name": [P, P],
     "GxB_Global_set_int": [ctypes.c_char_p, L], "GxB_Global_get_int": [ctypes.c_char_p, P],
+    "GxB_MatrixMarket_read_coo": [ctypes.c_char_p, P, P, P, P, P, P, P], "GxB_MatrixMarket_free": [P],
     "GrB_Descriptor_new": [P], "GrB_Descriptor_set": [P, E, E], "GrB_Descriptor_free": [P],
     "GrB_Matrix_new": [P, P, I, I], "GrB_Matrix_dup": [P, P], "GrB_Matrix_clear": [P],
     "GrB_Matrix_nrows": [P, P], "GrB_Matrix_ncols": [P, P], "GrB_Matrix_nvals": [P, P],

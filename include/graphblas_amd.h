@@ -304,6 +304,15 @@ GrB_Info GxB_Matrix_rmat(GrB_Matrix *A, int scale, int edge_factor, uint64_t see
                          GrB_Index row_end);
 /* Force the cached CSC (transpose) of A to be built now (outside timed regions). */
 GrB_Info GxB_Matrix_prepare_transpose(GrB_Matrix A);
+/* Matrix Market coordinate reader (host, multithreaded; replaces the scipy /
+ * fast_matrix_market parse behind reference graphblas/io/_matrixmarket.py:6-61).
+ * Returns 0-based COO arrays allocated with malloc (free each with
+ * GxB_MatrixMarket_free) for GrB_Matrix_build_*: pattern -> BOOL (X all 1),
+ * integer -> INT64, real -> FP64 (*type_code: gbamd_type_code); symmetric and
+ * skew-symmetric files come back expanded. */
+GrB_Info GxB_MatrixMarket_read_coo(const char *path, GrB_Index *nrows, GrB_Index *ncols, GrB_Index *nvals,
+                                   int *type_code, GrB_Index **I, GrB_Index **J, void **X);
+GrB_Info GxB_MatrixMarket_free(void *p);
 /* Backend selection knobs for benchmarking ablations: 0 = automatic. */
 GrB_Info GxB_Global_set_int(const char *key, int64_t value);
 GrB_Info GxB_Global_get_int(const char *key, int64_t *value);
