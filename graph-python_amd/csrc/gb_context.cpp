@@ -394,7 +394,15 @@ GrB_Info GrB_Monoid_free(GrB_Monoid *m) {
     return GrB_SUCCESS;
 }
 GrB_Info GrB_Semiring_free(GrB_Semiring *s) {
-    (void)s;
+    if (s && *s && (*s)->magic == GB_MAGIC && (*s)->user) {
+        (*s)->magic = GB_FREED;
+        delete *s;
+        *s = nullptr;
+    }
+    return GrB_SUCCESS;
+}
+GrB_Info GrB_UnaryOp_free(GrB_UnaryOp *op) {
+    (void)op;
     return GrB_SUCCESS;
 }
 GrB_Info GxB_Semiring_add(GrB_Monoid *add, GrB_Semiring s) {

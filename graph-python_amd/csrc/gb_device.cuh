@@ -225,6 +225,56 @@ GB_HD T gb_binop(int op, T x, T y) {
     }
 }
 
+// z = op(x) for the builtin unary operators (x, z of type T)
+template <class T>
+GB_HD T gb_unop(int op, T x) {
+    if constexpr (std::is_same<T, bool>::value) {
+        switch (op) {
+        case GBAMD_UOP_LNOT: case GBAMD_UOP_BNOT: return !x;
+        case GBAMD_UOP_ONE: return true;
+        case GBAMD_UOP_MINV: return true;  // SuiteSparse: MINV_BOOL(x) = true
+        default: return x;                 // IDENTITY, AINV, ABS
+        }
+    } else {
+        switch (op) {
+        case GBAMD_UOP_IDENTITY: return x;
+        case GBAMD_UOP_AINV: return gb_wrap_sub((T)0, x);
+        case GBAMD_UOP_MINV:
+            if constexpr (gb_traits<T>::is_int) return gb_idiv((T)1, x);
+            else return (T)1 / x;
+        case GBAMD_UOP_ABS:
+            if constexpr (std::is_unsigned<T>::value) return x;
+            else if constexpr (std::is_floating_point<T>::value) return (T)fabs(x);
+            else return x < 0 ? gb_wrap_sub((T)0, x) : x;
+        case GBAMD_UOP_LNOT: return x == (T)0 ? (T)1 : (T)0;
+        case GBAMD_UOP_ONE: return (T)1;
+        default: break;
+        }
+        if constexpr (gb_traits<T>::is_int) {
+            using U = typename std::make_unsigned<T>::type;
+            if (op == GBAMD_UOP_BNOT) return (T)(U)~(U)x;
+            return x;
+        } else {
+            switch (op) {
+            case GBAMD_UOP_SQRT: return (T)sqrt((double)x);
+            case GBAMD_UOP_LOG: return (T)log((double)x);
+            case GBAMD_UOP_LOG2: return (T)log2((double)x);
+            case GBAMD_UOP_LOG10: return (T)log10((double)x);
+            case GBAMD_UOP_EXP: return (T)exp((double)x);
+            case GBAMD_UOP_EXP2: return (T)exp2((double)x);
+            case GBAMD_UOP_FLOOR: return (T)floor((double)x);
+            case GBAMD_UOP_CEIL: return (T)ceil((double)x);
+            case GBAMD_UOP_ROUND: return (T)round((double)x);
+            case GBAMD_UOP_TRUNC: return (T)trunc((double)x);
+            case GBAMD_UOP_SIN: return (T)sin((double)x);
+            case GBAMD_UOP_COS: return (T)cos((double)x);
+            case GBAMD_UOP_TAN: return (T)tan((double)x);
+            default: return x;
+            }
+        }
+    }
+}
+
 GB_HD int64_t gb_posop(int op, int64_t i, int64_t k, int64_t j) {
     switch (op) {
     case GBAMD_OP_FIRSTI: return i;

@@ -32,6 +32,12 @@ struct GB_BinaryOp_opaque {
     GrB_Type xtype, ytype, ztype;  // xtype == nullptr: positional op
     const char *name;
 };
+struct GB_UnaryOp_opaque {
+    uint64_t magic;
+    int opcode;
+    GrB_Type xtype, ztype;
+    const char *name;
+};
 struct GB_Monoid_opaque {
     uint64_t magic;
     int mcode;
@@ -44,6 +50,7 @@ struct GB_Semiring_opaque {
     GrB_Monoid add;
     GrB_BinaryOp mul;
     const char *name;
+    bool user;  // created by GrB_Semiring_new (heap), freed by GrB_Semiring_free
 };
 struct GB_Descriptor_opaque {
     uint64_t magic;

@@ -644,6 +644,170 @@ static void matrix_assign_scalar(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, const
 }
 
 // ================================================================== C API
+// ================================================================== apply
+// z = op(x) (kind 0), op(s, x) (kind 1, BinaryOp1st), op(x, s) (kind 2, BinaryOp2nd)
+// over the n stored values (n = 1 for iso inputs): structure is not touched.
+template <class X, class Z>
+__global__ void k_apply(int64_t n, int kind, int op, const X *__restrict__ in, X s, Z *__restrict__ out) {
+    OPS_STRIDE(i, n) {
+        X x = in[i];
+        if (kind == 0) out[i] = gb_cast<Z, X>(gb_unop<X>(op, x));
+        else if (kind == 1) out[i] = gb_binop_z<X, Z>(op, s, x, 0, 0, 0);
+        else out[i] = gb_binop_z<X, Z>(op, x, s, 0, 0, 0);
+    }
+}
+
+// kind 0: uop; kind 1/2: bop with the bound scalar *sval (type scode)
+static void do_apply(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, int kind, GrB_UnaryOp uop, GrB_BinaryOp bop,
+                     const void *sval, int scode, GB_Obj *A, const gb_desc &d) {
+    check_binop(accum, true);
+    int xcode, zcode, opcode;
+    if (kind == 0) {
+        GB_REQUIRE(uop, GrB_NULL_POINTER, "operator is NULL");
+        GB_REQUIRE(uop->magic == GB_MAGIC, GrB_UNINITIALIZED_OBJECT, "invalid operator");
+        xcode = uop->xtype->code;
+        zcode = uop->ztype->code;
+        opcode = uop->opcode;
+    } else {
+        check_binop(bop, false);
+        GB_REQUIRE(bop->xtype != nullptr, GrB_NOT_IMPLEMENTED, "positional operator in apply");
+        xcode = bop->xtype->code;
+        zcode = bop->ztype->code;
+        opcode = bop->opcode;
+    }
+    // the bound scalar, cast to the operator's input type
+    char sx[16] = {0};
+    if (kind != 0) {
+        gb_with_type(scode, [&](auto sv) {
+            using S = decltype(sv);
+            S v;
+            memcpy(&v, sval, sizeof(S));
+            gb_with_type(xcode, [&](auto xv) {
+                using X = decltype(xv);
+                X c = gb_cast<X, S>(v);
+                memcpy(sx, &c, sizeof(X));
+            });
+        });
+    }
+    auto launch = [&](int64_t n, const void *in, void *out) {
+        dispatch_xz(xcode, zcode, [&](auto x, auto z) {
+            using X = decltype(x);
+            using Z = decltype(z);
+            X s;
+            memcpy(&s, sx, sizeof(X));
+            if (n)
+                hipLaunchKernelGGL((k_apply<X, Z>), dim3(ops_grid(n)), dim3(OPS_BLOCK), 0, gb_stream(), n, kind,
+                                   opcode, (const X *)in, s, (Z *)out);
+        });
+        GB_LAUNCH_CHECK();
+    };
+    const size_t zs = gb_type_size(zcode);
+    if (C->kind != GB_KIND_MATRIX) {
+        GB_REQUIRE(A->nrows == C->nrows && ncols_of(A) == 1, GrB_DIMENSION_MISMATCH, "vector sizes do not match");
+        gb_bitmap_view uv;
+        gb_get_bitmap(uv, A);
+        gb_scratch s;
+        const void *xin = gb_bitmap_vals_as(uv, xcode, s);
+        gb_vec_result T;
+        T.n = uv.n;
+        T.tcode = zcode;
+        T.iso = uv.iso;
+        const int64_t nw = gb_words(uv.n);
+        T.bits = gb_malloc_n<uint64_t>(std::max<int64_t>(nw, 1));
+        if (nw) gb_copy_d2d(T.bits, uv.bits, nw * sizeof(uint64_t));
+        const int64_t nv = uv.iso ? 1 : uv.n;
+        T.dense = gb_malloc(std::max<int64_t>(nv, 1) * zs);
+        launch(nv, xin, T.dense);
+        T.d_nvals = gb_malloc_n<int64_t>(1);
+        if (uv.count) gb_copy_d2d(T.d_nvals, uv.count, sizeof(int64_t));
+        else gb_bitmap_count(T.bits, T.n, T.d_nvals);
+        gb_writeback_vector(C, T, M, d, accum, false);
+        return;
+    }
+    gb_csr_view v;
+    if (d.tran0) gb_get_csc(v, A);
+    else gb_get_csr(v, A);
+    GB_REQUIRE(v.nrows == C->nrows && v.ncols == C->ncols, GrB_DIMENSION_MISMATCH, "matrix dimensions do not match");
+    gb_scratch s;
+    const void *xin = gb_view_vals_as(v, xcode, s);
+    gb_mat_result T;
+    T.nrows = v.nrows;
+    T.ncols = v.ncols;
+    T.nvals = v.nvals;
+    T.tcode = zcode;
+    T.iso = v.iso;
+    T.rowptr = gb_malloc_n<int64_t>(v.nrows + 1);
+    gb_copy_d2d(T.rowptr, v.rowptr, (v.nrows + 1) * sizeof(int64_t));
+    T.colidx = gb_malloc_n<int32_t>(std::max<int64_t>(v.nvals, 1));
+    if (v.nvals) gb_copy_d2d(T.colidx, v.colidx, v.nvals * sizeof(int32_t));
+    const int64_t nv = v.iso ? (v.nvals ? 1 : 0) : v.nvals;
+    T.vals = gb_malloc(std::max<int64_t>(nv, 1) * zs);
+    launch(nv, xin, T.vals);
+    gb_writeback_matrix(C, T, M, d, accum);
+}
+
+// ================================================================== reduce to vector
+static GrB_BinaryOp first_of(int code) {
+    void *h;
+    int kind;
+    std::string name = std::string("GrB_FIRST_") + gb_type_name(code);
+    GxB_builtin_lookup(&h, &kind, name.c_str());
+    return (GrB_BinaryOp)h;
+}
+
+static void do_reduce_rows(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Monoid monoid, GB_Obj *A,
+                           const gb_desc &d) {
+    GB_REQUIRE(monoid, GrB_NULL_POINTER, "monoid is NULL");
+    GB_REQUIRE(monoid->magic == GB_MAGIC, GrB_UNINITIALIZED_OBJECT, "invalid monoid");
+    GB_REQUIRE(A->kind == GB_KIND_MATRIX, GrB_INVALID_OBJECT, "reduce input must be a matrix");
+    const int code = monoid->type->code;
+    // w = A' (monoid.FIRST) ones: the product is A'(i,k); the iso-full vector only supplies structure
+    GB_Semiring_opaque sr{GB_MAGIC, monoid, first_of(code), "reduce", false};
+    const int64_t k = d.tran0 ? A->nrows : A->ncols;
+    GrB_Vector u = nullptr;
+    GrB_Info info = GrB_Vector_new(&u, monoid->type, (GrB_Index)k);
+    GB_REQUIRE(info == GrB_SUCCESS, info, "cannot allocate the reduction vector");
+    struct Free {
+        GrB_Vector *u;
+        ~Free() { GrB_Vector_free(u); }
+    } fr{&u};
+    char one[16] = {0};
+    gb_with_type(code, [&](auto z) {
+        using Z = decltype(z);
+        Z v = (Z)1;
+        memcpy(one, &v, sizeof(Z));
+    });
+    vector_assign_scalar(OBJ(u), nullptr, nullptr, one, code, GrB_ALL, k, gb_desc());
+    gb_desc dd = d;
+    dd.tran1 = false;
+    do_spmv(w, mask, accum, &sr, A, OBJ(u), dd, false);
+}
+
+static GrB_Monoid monoid_of_binop(GrB_BinaryOp op) {
+    check_binop(op, false);
+    GB_REQUIRE(op->xtype != nullptr && op->xtype == op->ztype, GrB_DOMAIN_MISMATCH,
+               "reduce requires a BinaryOp that is a monoid");
+    static const struct {
+        int opcode;
+        const char *pre, *mid;
+    } tab[] = {{GBAMD_OP_PLUS, "GrB_PLUS_MONOID_", nullptr},   {GBAMD_OP_TIMES, "GrB_TIMES_MONOID_", nullptr},
+               {GBAMD_OP_MIN, "GrB_MIN_MONOID_", nullptr},     {GBAMD_OP_MAX, "GrB_MAX_MONOID_", nullptr},
+               {GBAMD_OP_ANY, "GxB_ANY_", "_MONOID"},          {GBAMD_OP_LOR, "GrB_LOR_MONOID_", nullptr},
+               {GBAMD_OP_LAND, "GrB_LAND_MONOID_", nullptr},   {GBAMD_OP_LXOR, "GrB_LXOR_MONOID_", nullptr},
+               {GBAMD_OP_LXNOR, "GrB_LXNOR_MONOID_", nullptr}, {GBAMD_OP_BOR, "GxB_BOR_", "_MONOID"},
+               {GBAMD_OP_BAND, "GxB_BAND_", "_MONOID"},        {GBAMD_OP_BXOR, "GxB_BXOR_", "_MONOID"},
+               {GBAMD_OP_BXNOR, "GxB_BXNOR_", "_MONOID"}};
+    for (auto &t : tab) {
+        if (t.opcode != op->opcode) continue;
+        std::string name = std::string(t.pre) + gb_type_name(op->ztype->code) + (t.mid ? t.mid : "");
+        void *h = nullptr;
+        int kind = -1;
+        if (GxB_builtin_lookup(&h, &kind, name.c_str()) == GrB_SUCCESS && kind == 2) return (GrB_Monoid)h;
+    }
+    gb_throw(GrB_DOMAIN_MISMATCH, "reduce requires a BinaryOp that is a monoid");
+    return nullptr;
+}
+
 extern "C" {
 
 GrB_Info GrB_mxm(GrB_Matrix C, const GrB_Matrix Mask, const GrB_BinaryOp accum, const GrB_Semiring op,
@@ -828,6 +992,43 @@ GrB_Info GrB_Vector_reduce_Monoid_Scalar(GrB_Scalar s, const GrB_BinaryOp accum,
                                          const GrB_Vector u, const GrB_Descriptor desc) {
     return GrB_Matrix_reduce_Monoid_Scalar(s, accum, monoid, (GrB_Matrix)u, desc);
 }
+GrB_Info GrB_Matrix_reduce_Monoid(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum,
+                                  const GrB_Monoid monoid, const GrB_Matrix A, const GrB_Descriptor desc) {
+    return gb_api(OBJ(w), [&] {
+        do_reduce_rows(gb_obj_check(w), gb_obj_check(mask, true), accum, monoid, gb_obj_check(A),
+                       gb_read_desc(desc));
+    });
+}
+GrB_Info GrB_Matrix_reduce_BinaryOp(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum,
+                                    const GrB_BinaryOp op, const GrB_Matrix A, const GrB_Descriptor desc) {
+    return gb_api(OBJ(w), [&] {
+        do_reduce_rows(gb_obj_check(w), gb_obj_check(mask, true), accum, monoid_of_binop(op), gb_obj_check(A),
+                       gb_read_desc(desc));
+    });
+}
+GrB_Info GrB_Vector_apply(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum, const GrB_UnaryOp op,
+                          const GrB_Vector u, const GrB_Descriptor desc) {
+    return gb_api(OBJ(w), [&] {
+        do_apply(gb_obj_check(w), gb_obj_check(mask, true), accum, 0, op, nullptr, nullptr, 0, gb_obj_check(u),
+                 gb_read_desc(desc));
+    });
+}
+GrB_Info GrB_Matrix_apply(GrB_Matrix C, const GrB_Matrix Mask, const GrB_BinaryOp accum, const GrB_UnaryOp op,
+                          const GrB_Matrix A, const GrB_Descriptor desc) {
+    return gb_api(OBJ(C), [&] {
+        do_apply(gb_obj_check(C), gb_obj_check(Mask, true), accum, 0, op, nullptr, nullptr, 0, gb_obj_check(A),
+                 gb_read_desc(desc));
+    });
+}
+GrB_Info GrB_Semiring_new(GrB_Semiring *semiring, GrB_Monoid add, GrB_BinaryOp multiply) {
+    if (!semiring || !add || !multiply) return GrB_NULL_POINTER;
+    if (add->magic != GB_MAGIC || multiply->magic != GB_MAGIC) return GrB_UNINITIALIZED_OBJECT;
+    if (multiply->ztype != add->type) return GrB_DOMAIN_MISMATCH;
+    GB_Semiring_opaque *s = new (std::nothrow) GB_Semiring_opaque{GB_MAGIC, add, multiply, "user_semiring", true};
+    if (!s) return GrB_OUT_OF_MEMORY;
+    *semiring = s;
+    return GrB_SUCCESS;
+}
 
 #define GB_DEFINE_TYPED_OPS(T, ctype)                                                                          \
     GrB_Info GrB_Vector_assign_##T(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum, ctype x,   \
@@ -875,6 +1076,38 @@ GrB_Info GrB_Vector_reduce_Monoid_Scalar(GrB_Scalar s, const GrB_BinaryOp accum,
     GrB_Info GrB_Matrix_reduce_##T(ctype *c, const GrB_BinaryOp accum, const GrB_Monoid monoid,              \
                                    const GrB_Matrix A, const GrB_Descriptor desc) {                          \
         return GrB_Vector_reduce_##T(c, accum, monoid, (GrB_Vector)A, desc);                                 \
+    }                                                                                                        \
+    GrB_Info GrB_Vector_apply_BinaryOp1st_##T(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum,  \
+                                              const GrB_BinaryOp op, ctype x, const GrB_Vector u,            \
+                                              const GrB_Descriptor desc) {                                   \
+        return gb_api(OBJ(w), [&] {                                                                          \
+            do_apply(gb_obj_check(w), gb_obj_check(mask, true), accum, 1, nullptr, op, &x, GBAMD_T_##T,      \
+                     gb_obj_check(u), gb_read_desc(desc));                                                   \
+        });                                                                                                  \
+    }                                                                                                        \
+    GrB_Info GrB_Vector_apply_BinaryOp2nd_##T(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum,  \
+                                              const GrB_BinaryOp op, const GrB_Vector u, ctype y,            \
+                                              const GrB_Descriptor desc) {                                   \
+        return gb_api(OBJ(w), [&] {                                                                          \
+            do_apply(gb_obj_check(w), gb_obj_check(mask, true), accum, 2, nullptr, op, &y, GBAMD_T_##T,      \
+                     gb_obj_check(u), gb_read_desc(desc));                                                   \
+        });                                                                                                  \
+    }                                                                                                        \
+    GrB_Info GrB_Matrix_apply_BinaryOp1st_##T(GrB_Matrix C, const GrB_Matrix Mask, const GrB_BinaryOp accum,  \
+                                              const GrB_BinaryOp op, ctype x, const GrB_Matrix A,            \
+                                              const GrB_Descriptor desc) {                                   \
+        return gb_api(OBJ(C), [&] {                                                                          \
+            do_apply(gb_obj_check(C), gb_obj_check(Mask, true), accum, 1, nullptr, op, &x, GBAMD_T_##T,      \
+                     gb_obj_check(A), gb_read_desc(desc));                                                   \
+        });                                                                                                  \
+    }                                                                                                        \
+    GrB_Info GrB_Matrix_apply_BinaryOp2nd_##T(GrB_Matrix C, const GrB_Matrix Mask, const GrB_BinaryOp accum,  \
+                                              const GrB_BinaryOp op, const GrB_Matrix A, ctype y,            \
+                                              const GrB_Descriptor desc) {                                   \
+        return gb_api(OBJ(C), [&] {                                                                          \
+            do_apply(gb_obj_check(C), gb_obj_check(Mask, true), accum, 2, nullptr, op, &y, GBAMD_T_##T,      \
+                     gb_obj_check(A), gb_read_desc(desc));                                                   \
+        });                                                                                                  \
     }
 
 GB_FOR_EACH_TYPE(GB_DEFINE_TYPED_OPS)

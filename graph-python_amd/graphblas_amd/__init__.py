@@ -22,7 +22,7 @@ from .exceptions import (DimensionMismatch, DomainMismatch, EmptyObject, Graphbl
                          NotImplementedException, NoValue, NullPointer, OutOfMemory, OutputNotEmpty,
                          Panic, UninitializedObject)
 from .matrix import Matrix, MatrixExpression, TransposedMatrix
-from .operator import binary, monoid, op, semiring
+from .operator import binary, monoid, op, semiring, unary
 from .scalar import Scalar, ScalarExpression
 from .vector import Vector, VectorExpression
 
@@ -62,7 +62,8 @@ def wait():
 
 
 __all__ = ["Matrix", "Vector", "Scalar", "TransposedMatrix", "Recorder", "binary", "monoid", "semiring",
-           "op", "dtypes", "init", "replace", "backend", "lib"]
+           "op", "unary", "agg", "dtypes", "init", "replace", "backend", "lib"]
 
 from . import dtypes  # noqa: E402
 from . import io  # noqa: E402,F401
+from .agg import agg  # noqa: E402

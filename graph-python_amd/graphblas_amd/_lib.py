@@ -52,6 +52,9 @@ _SIGS = {
     "GrB_Vector_assign": [P, P, P, P, P, I, P], "GrB_Matrix_assign": [P, P, P, P, P, I, P, I, P],
     "GrB_Matrix_reduce_Monoid_Scalar": [P] * 5, "GrB_Vector_reduce_Monoid_Scalar": [P] * 5,
     "GrB_transpose": [P] * 5,
+    "GrB_Matrix_reduce_Monoid": [P] * 6, "GrB_Matrix_reduce_BinaryOp": [P] * 6,
+    "GrB_Vector_apply": [P] * 6, "GrB_Matrix_apply": [P] * 6,
+    "GrB_Semiring_new": [P, P, P], "GrB_UnaryOp_free": [P],
     "GxB_Matrix_device_view": [P, P], "GxB_Vector_device_view": [P, P],
     "GxB_Vector_device_touch": [P], "GxB_Matrix_prepare_transpose": [P],
     "GxB_Matrix_rmat": [P, E, E, U, E, U, I, I],
@@ -78,6 +81,10 @@ for _t in TYPE_NAMES:
         f"GrB_Vector_reduce_{_t}": [P, P, P, P, P],
         f"GrB_Scalar_setElement_{_t}": [P, _T],
         f"GrB_Scalar_extractElement_{_t}": [P, P],
+        f"GrB_Vector_apply_BinaryOp1st_{_t}": [P, P, P, P, _T, P, P],
+        f"GrB_Vector_apply_BinaryOp2nd_{_t}": [P, P, P, P, P, _T, P],
+        f"GrB_Matrix_apply_BinaryOp1st_{_t}": [P, P, P, P, _T, P, P],
+        f"GrB_Matrix_apply_BinaryOp2nd_{_t}": [P, P, P, P, P, _T, P],
     })
 
 # GrB_Info codes (C API 2.0; include/graphblas_amd.h)
@@ -138,7 +145,7 @@ class _Lib:
     def __dir__(self):
         names = list(_SIGS) + list(INFO) + list(ENUMS)
         names += [f"GrB_{t}" for t in TYPE_NAMES]
-        names += list(_builtins.BINOPS) + list(_builtins.MONOIDS) + list(_builtins.DESCRIPTORS.values())
+        names += list(_builtins.BINOPS) + list(_builtins.UNOPS) + list(_builtins.MONOIDS) + list(_builtins.DESCRIPTORS.values())
         for k, v in _builtins.SEMIRINGS.items():
             names.append(k)
             names.extend(v[2])

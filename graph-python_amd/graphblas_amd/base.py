@@ -367,6 +367,16 @@ class BaseType:
 
         return _matmul_infix_expr(other, self)
 
+    def __and__(self, other):
+        from .infix import _ewise_infix_expr
+
+        return _ewise_infix_expr(self, other, "ewise_mult")
+
+    def __or__(self, other):
+        from .infix import _ewise_infix_expr
+
+        return _ewise_infix_expr(self, other, "ewise_add")
+
     def __imatmul__(self, other):
         self << self @ other
         return self

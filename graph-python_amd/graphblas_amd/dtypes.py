@@ -88,10 +88,15 @@ def lookup_dtype(key):
     raise ValueError(f"Unknown dtype: {key} of type {type(key)}")
 
 
-def unify(type1, type2):
+def unify(type1, type2, *, is_left_scalar=False, is_right_scalar=False):
     """A type that can hold both (numpy promotion, reference core/dtypes.py:377-394)."""
     if type1 is type2:
         return type1
+    if is_left_scalar:
+        if not is_right_scalar:
+            return lookup_dtype(np.result_type(np.array(0, type1.np_type), type2.np_type))
+    elif is_right_scalar:
+        return lookup_dtype(np.result_type(type1.np_type, np.array(0, type2.np_type)))
     return lookup_dtype(np.promote_types(type1.np_type, type2.np_type))
 
 

@@ -13,7 +13,9 @@ class InfixExpr:
         return getattr(self.left, self.method)(self.right, op)
 
     def _to_expr(self):
-        return self._with_op(_op.semiring.plus_times)
+        default = {"ewise_mult": _op.binary.times, "ewise_add": _op.monoid.plus}.get(self.method,
+                                                                                   _op.semiring.plus_times)
+        return self._with_op(default)
 
     def new(self, dtype=None, *, mask=None, name=None, **opts):
         return self._to_expr().new(dtype, mask=mask, name=name, **opts)
@@ -58,3 +60,10 @@ def _matmul_infix_expr(left, right):
     expr = InfixExpr(left, right, method)
     expr._to_expr()  # shape check now (reference core/infix.py:492)
     return expr
+
+
+def _ewise_infix_expr(left, right, method):
+    """`x & y` (eWiseMult) / `x | y` (eWiseAdd) (reference core/infix.py:251-259, 388-397)."""
+    if getattr(left, "ndim", None) is None or getattr(right, "ndim", None) is None:
+        return NotImplemented
+    return InfixExpr(left, right, method)

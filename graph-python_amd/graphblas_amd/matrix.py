@@ -92,6 +92,12 @@ class Matrix(BaseType):
         return TransposedMatrix(self)
 
     @property
+    def ss(self):
+        from .ss import MatrixSS
+
+        return MatrixSS(self)
+
+    @property
     def S(self):
         return StructuralMask(self)
 
@@ -286,11 +292,16 @@ class Matrix(BaseType):
         return _ewise(self, other, op if op is not None else _op.monoid.plus, "add")
 
     def reduce_scalar(self, op=None, *, allow_empty=True):
-        from .scalar import ScalarExpression
+        return _reduce_scalar(self, op, allow_empty)
 
-        op = _op.get_typed_op(op if op is not None else _op.monoid.plus, self.dtype, kind="monoid")
-        return ScalarExpression("reduce_scalar", "GrB_Matrix_reduce_Monoid_Scalar", [self], op=op,
-                                allow_empty=allow_empty)
+    def reduce_rowwise(self, op=None):
+        return _reduce_rows(self, op, columnwise=False)
+
+    def reduce_columnwise(self, op=None):
+        return _reduce_rows(self, op, columnwise=True)
+
+    def apply(self, op, right=None, *, left=None):
+        return _apply_expr(self, op, right, left)
 
     def isequal(self, other, *, check_dtype=False):
         """reference core/matrix.py:357-398"""
@@ -460,6 +471,18 @@ class TransposedMatrix:
     def power(self, n, op=None):
         return self.new().power(n, op)
 
+    def reduce_rowwise(self, op=None):
+        return _reduce_rows(self, op, columnwise=False)
+
+    def reduce_columnwise(self, op=None):
+        return _reduce_rows(self, op, columnwise=True)
+
+    def reduce_scalar(self, op=None, *, allow_empty=True):
+        return self._matrix.reduce_scalar(op, allow_empty=allow_empty)
+
+    def apply(self, op, right=None, *, left=None):
+        return _apply_expr(self, op, right, left)
+
     def to_coo(self, *args, **kw):
         r, c, v = self._matrix.to_coo(*args, **kw)
         o = np.lexsort((r, c))
@@ -477,6 +500,103 @@ class TransposedMatrix:
         from .infix import _matmul_infix_expr
 
         return _matmul_infix_expr(other, self)
+
+
+def _is_agg(op):
+    return getattr(op, "opclass", None) == "Aggregator"
+
+
+def _reduce_rows(A, op, *, columnwise):
+    """A.reduce_rowwise / reduce_columnwise (reference core/matrix.py:2556-2623): a monoid (or a
+    BinaryOp that is one) -> GrB_Matrix_reduce_Monoid (desc INP0=TRAN for columns of A, rows of
+    A.T); an Aggregator -> its semiring lowering (agg.py)."""
+    from .vector import VectorExpression
+
+    if op is None:
+        op = _op.monoid.plus
+    size = A.ncols if columnwise else A.nrows
+    if _is_agg(op):
+        from .agg import reduce_rowwise_recipe
+
+        typed = op[A.dtype] if op.opclass == "Aggregator" and not hasattr(op, "parent") else op
+        return VectorExpression("reduce_columnwise" if columnwise else "reduce_rowwise", None,
+                                [A, reduce_rowwise_recipe, (A, typed, columnwise)],
+                                dtype=typed.return_type, size=size)
+    t = _op.get_typed_op(op, A.dtype, kind="monoid")
+    if t.opclass == "BinaryOp":
+        mon = getattr(_op.monoid, t.parent.name, None)
+        if mon is None or t.type not in mon._typed:
+            raise TypeError(f"{op!r} is not a monoid; reduce needs a Monoid")
+        t = mon[t.type]
+    if t.opclass != "Monoid":
+        raise TypeError(f"Expected a Monoid or Aggregator, got {t.opclass}")
+    a, at = _unwrap(A)
+    return VectorExpression("reduce_columnwise" if columnwise else "reduce_rowwise", "GrB_Matrix_reduce_Monoid",
+                            [a], op=t, at=(at != columnwise), size=size)
+
+
+def _reduce_scalar(x, op, allow_empty):
+    """Vector.reduce / Matrix.reduce_scalar: monoids -> GrB_*_reduce_Monoid_Scalar; Aggregators ->
+    the two-SpMV lowering of reference core/operator/agg.py:229-276."""
+    from .scalar import ScalarExpression
+
+    if op is None:
+        op = _op.monoid.plus
+    if _is_agg(op):
+        from .agg import reduce_scalar_recipe
+
+        typed = op[x.dtype] if not hasattr(op, "parent") else op
+        if not allow_empty:
+            if typed.parent._monoid is None:
+                raise ValueError("allow_empty=False not allowed when using Aggregators")
+            return _reduce_scalar(x, typed.parent._monoid[typed.type], allow_empty)
+        return ScalarExpression("reduce", None, [x, reduce_scalar_recipe, (x, typed)],
+                                dtype=typed.return_type)
+    op = _op.get_typed_op(op, x.dtype, kind="monoid")
+    if op.opclass == "BinaryOp":
+        op = getattr(_op.monoid, op.parent.name)[op.type]
+    kind = "Matrix" if x.ndim == 2 else "Vector"
+    return ScalarExpression("reduce_scalar" if kind == "Matrix" else "reduce",
+                            f"GrB_{kind}_reduce_Monoid_Scalar", [x], op=op, allow_empty=allow_empty)
+
+
+def _apply_expr(x, op, right, left):
+    """x.apply(op[, right= | left=]) (reference core/vector.py:1311-1460, core/matrix.py:2297-2447):
+    a UnaryOp -> GrB_*_apply; a BinaryOp with a bound scalar -> GrB_*_apply_BinaryOp{1st,2nd}_<T>."""
+    from .scalar import Scalar
+    from .vector import VectorExpression
+
+    kind = "Vector" if x.ndim == 1 else "Matrix"
+    src, at = _unwrap(x) if kind == "Matrix" else (x, False)
+
+    def mk(cf, args, t):
+        if kind == "Vector":
+            return VectorExpression("apply", cf, args, op=t, size=x.size)
+        return MatrixExpression("apply", cf, args, op=t, at=at, nrows=x.nrows, ncols=x.ncols)
+
+    if left is None and right is None:
+        t = _op.get_typed_op(op, x.dtype, kind="unary")
+        if t.opclass != "UnaryOp":
+            raise TypeError(f"Bad type for argument `op`: expected UnaryOp, got {t.opclass}")
+        return mk(f"GrB_{kind}_apply", [src], t)
+    if left is not None and right is not None:
+        raise TypeError("Cannot provide both `left` and `right` to apply")
+    val = left if right is None else right
+    sc = val if isinstance(val, Scalar) else Scalar.from_value(val)
+    if right is None:
+        t = _op.get_typed_op(op, sc.dtype, x.dtype, kind="binary", is_left_scalar=True)
+    else:
+        t = _op.get_typed_op(op, x.dtype, sc.dtype, kind="binary", is_right_scalar=True)
+    if t.opclass == "Monoid":
+        t = getattr(_op.binary, t.parent.name)[t.type]
+    elif t.opclass != "BinaryOp":
+        raise TypeError(f"Bad type for argument `op`: expected BinaryOp, got {t.opclass}")
+    if t.is_positional:
+        raise NotImplementedError("positional operators in apply")
+    cv = sc.value
+    if right is None:
+        return mk(f"GrB_{kind}_apply_BinaryOp1st_{sc.dtype.name}", [cv, src], t)
+    return mk(f"GrB_{kind}_apply_BinaryOp2nd_{sc.dtype.name}", [src, cv], t)
 
 
 def _unwrap(x):

@@ -46,8 +46,8 @@ class TypedOp:
     def __repr__(self):
         return f"{self.opclass.lower()}.{self.name}[{self.type}]"
 
-    def __call__(self, expr):
-        return _call_op(self, expr)
+    def __call__(self, expr, right=None):
+        return _call_op(self, expr, right)
 
 
 class OpBase:
@@ -79,12 +79,16 @@ class OpBase:
     def __repr__(self):
         return f"{self.opclass.lower()}.{self.name}"
 
-    def __call__(self, expr):
-        return _call_op(self, expr)
+    def __call__(self, expr, right=None):
+        return _call_op(self, expr, right)
 
 
 class BinaryOp(OpBase):
     opclass = "BinaryOp"
+
+
+class UnaryOp(OpBase):
+    opclass = "UnaryOp"
 
 
 class Monoid(OpBase):
@@ -105,6 +109,7 @@ class _Namespace(types.SimpleNamespace):
 
 
 binary = _Namespace()
+unary = _Namespace()
 monoid = _Namespace()
 semiring = _Namespace()
 
@@ -128,6 +133,14 @@ for _gb, (_op, _x, _z) in _builtins.BINOPS.items():
     if _dt in _o._typed and _o._typed[_dt].gb_name.startswith("GrB_"):
         continue
     _o._add(TypedOp(_o, _pyname, _dt, lookup_dtype(_z), _gb, "BinaryOp"))
+
+for _gb, (_op, _t) in _builtins.UNOPS.items():
+    _pyname = _op.lower()
+    _o = _get(unary, UnaryOp, _pyname)
+    _dt = lookup_dtype(_t)
+    if _dt in _o._typed and _o._typed[_dt].gb_name.startswith("GrB_"):
+        continue
+    _o._add(TypedOp(_o, _pyname, _dt, _dt, _gb, "UnaryOp"))
 
 for _gb, (_m, _t, _bop) in _builtins.MONOIDS.items():
     _pyname = "eq" if _gb == "GxB_EQ_BOOL_MONOID" else _m.lower()
@@ -197,7 +210,69 @@ for _opname, _target in [("max_first", "lor_first"), ("max_second", "lor_second"
 for _r in ["firsti", "firsti1", "firstj", "firstj1", "secondi", "secondi1", "secondj", "secondj1"]:
     _coerce(getattr(binary, _r), _POSDT, INT64)
 
-op = _Namespace(**{**binary.__dict__, **monoid.__dict__, **semiring.__dict__})
+# monoid coercions (reference core/operator/monoid.py:396-431): bool max/min/times are lor/land/land;
+# the logical monoids on numeric inputs use the BOOL monoid (values cast to bool)
+for _name, _target in [("max", "lor"), ("min", "land"), ("times", "land")]:
+    _a, _b = getattr(monoid, _name), getattr(monoid, _target)
+    if BOOL not in _a._typed:
+        _a._typed[BOOL] = _b._typed[BOOL]
+        _a.types[BOOL] = BOOL
+        _a.coercions[BOOL] = BOOL
+for _name in ["lor", "land", "lxnor", "lxor"]:
+    _a = getattr(monoid, _name)
+    for _dt in _NOTBOOL:
+        if _dt not in _a._typed:
+            _a._typed[_dt] = _a._typed[BOOL]
+            _a.types[_dt] = BOOL
+            _a.coercions[_dt] = BOOL
+
+# float-only unary ops on integer / bool inputs (reference core/operator/unary.py:381-428)
+_F32_FROM = [lookup_dtype(t) for t in ["BOOL", "INT8", "INT16", "UINT8", "UINT16"]]
+_F64_FROM = [lookup_dtype(t) for t in ["INT32", "INT64", "UINT32", "UINT64"]]
+for _u in unary.__dict__.values():
+    if lookup_dtype("FP64") in _u._typed and lookup_dtype("INT64") not in _u._typed:
+        _coerce(_u, _F32_FROM, lookup_dtype("FP32"))
+        _coerce(_u, _F64_FROM, lookup_dtype("FP64"))
+
+
+# ---- semirings python-graphblas builds from a monoid and a binary op when the library has no
+# builtin of that name (e.g. plus_pow for agg.sum_of_squares, reference core/operator/agg.py:266-276):
+# GrB_Semiring_new on the builtin pieces
+class _UserTypedSemiring(TypedOp):
+    __slots__ = ("_cell",)
+
+    def __init__(self, parent, name, dtype, ret, mon, bop):
+        import ctypes
+
+        self.parent, self.name, self.type, self.return_type = parent, name, dtype, ret
+        self.gb_name, self.opclass = name, "Semiring"
+        self._cell = ctypes.c_void_p()
+        rc = lib.GrB_Semiring_new(ctypes.byref(self._cell), mon.gb_obj, bop.gb_obj)
+        if rc != 0:
+            raise ValueError(f"GrB_Semiring_new({mon.gb_name}, {bop.gb_name}) failed ({rc})")
+        self.gb_obj = self._cell
+        self._monoid = mon.parent
+        self._binaryop = bop.parent
+
+
+def _user_semiring(mon_name, bop_name):
+    name = f"{mon_name}_{bop_name}"
+    if hasattr(semiring, name):
+        return getattr(semiring, name)
+    mon, bop = getattr(monoid, mon_name), getattr(binary, bop_name)
+    o = Semiring(name)
+    for dt, bt in bop._typed.items():
+        if dt in bop.coercions or bt.return_type not in mon._typed:
+            continue
+        mt = mon._typed[bt.return_type]
+        o._add(_UserTypedSemiring(o, name, dt, bt.return_type, mt, bt))
+    setattr(semiring, name, o)
+    return o
+
+
+_user_semiring("plus", "pow")
+
+op = _Namespace(**{**binary.__dict__, **unary.__dict__, **monoid.__dict__, **semiring.__dict__})
 
 _BINARY_STRINGS = {"+": "plus", "-": "minus", "*": "times", "/": "truediv", "==": "eq", "!=": "ne",
                    ">": "gt", "<": "lt", ">=": "ge", "<=": "le", "|": "lor", "&": "land",
@@ -210,14 +285,14 @@ def _from_string(s, kind):
     if name.endswith("]") and "[" in name:
         name, dt = name[:-1].split("[", 1)
     name = _BINARY_STRINGS.get(name, name).lower()
-    ns = {"binary": binary, "monoid": monoid, "semiring": semiring}[kind]
+    ns = {"binary": binary, "monoid": monoid, "semiring": semiring, "unary": unary}[kind]
     if not hasattr(ns, name):
         raise ValueError(f"Unknown {kind} string: {s!r}")
     obj = getattr(ns, name)
     return obj[dt] if dt else obj
 
 
-def get_typed_op(opobj, dtype, dtype2=None, *, kind=None):
+def get_typed_op(opobj, dtype, dtype2=None, *, kind=None, is_left_scalar=False, is_right_scalar=False):
     """Select the typed builtin for the given input dtypes (reference core/operator/utils.py:38-60)."""
     if isinstance(opobj, TypedOp):
         return opobj
@@ -227,7 +302,8 @@ def get_typed_op(opobj, dtype, dtype2=None, *, kind=None):
             return opobj
     if not isinstance(opobj, OpBase):
         raise TypeError(f"Unable to get typed operator from object with type {type(opobj)}")
-    dt = dtype if dtype2 is None else unify(dtype, dtype2)
+    dt = dtype if dtype2 is None else unify(dtype, dtype2, is_left_scalar=is_left_scalar,
+                                            is_right_scalar=is_right_scalar)
     if opobj.is_positional and dt not in opobj._typed:
         dt = INT64
     return opobj[dt]
@@ -239,10 +315,22 @@ def find_opclass(obj):
     return obj, "Unknown"
 
 
-def _call_op(opobj, expr):
-    """semiring(A @ B) / binary.plus(x | y) style (reference core/operator/base.py:110-161)."""
+def _call_op(opobj, expr, right=None):
+    """semiring(A @ B) / binary.plus(x | y) / binary.plus(x, 1) / unary.abs(x) style
+    (reference core/operator/base.py:110-161, binary.py:175-230)."""
     from .infix import InfixExpr
 
     if isinstance(expr, InfixExpr):
         return expr._with_op(opobj)
+    if right is not None:
+        lcol, rcol = getattr(expr, "ndim", None) is not None, getattr(right, "ndim", None) is not None
+        if lcol and rcol:
+            return expr.ewise_add(right, opobj)
+        if lcol:
+            return expr.apply(opobj, right=right)
+        if rcol:
+            return right.apply(opobj, left=expr)
+        raise TypeError(f"Bad types when calling {opobj!r}")
+    if opobj.opclass == "UnaryOp" and hasattr(expr, "apply"):
+        return expr.apply(opobj)
     raise TypeError(f"Bad type when calling {opobj!r}: {type(expr)}")

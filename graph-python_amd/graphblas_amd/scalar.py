@@ -141,7 +141,7 @@ class ScalarExpression(BaseExpression):
         if mask is not None:
             raise TypeError("Mask not allowed for Scalars")
         s = self.construct_output(dtype, name=name)
-        if not self._allow_empty and self.cfunc_name.endswith("reduce_Monoid_Scalar"):
+        if not self._allow_empty and self.cfunc_name and self.cfunc_name.endswith("reduce_Monoid_Scalar"):
             # allow_empty=False: C-scalar reduce, an empty input yields the monoid identity
             # (reference core/vector.py:1561 reduce -> GrB_Vector_reduce_<T>)
             A = self.args[0]

@@ -12,8 +12,8 @@ from .base import (BaseExpression, BaseType, StructuralMask, ValueMask, _autonam
                    descriptor_lookup)
 from .dtypes import BOOL, FP64, lookup_dtype
 from .exceptions import DimensionMismatch, NoValue, check_status_carg
-from .matrix import Matrix, MatrixExpression, TransposedMatrix, _binary_for, _CArray, _index_array, \
-    _values_dtype
+from .matrix import Matrix, MatrixExpression, TransposedMatrix, _apply_expr, _binary_for, _CArray, \
+    _index_array, _reduce_scalar, _values_dtype
 
 
 class Vector(BaseType):
@@ -49,6 +49,12 @@ class Vector(BaseType):
         return n.value
 
     _nvals = nvals
+
+    @property
+    def ss(self):
+        from .ss import VectorSS
+
+        return VectorSS(self)
 
     @property
     def S(self):
@@ -248,11 +254,10 @@ class Vector(BaseType):
         return VectorExpression(f"ewise_{kind}", cf, [self, other], op=op, size=self._size)
 
     def reduce(self, op=None, *, allow_empty=True):
-        from .scalar import ScalarExpression
+        return _reduce_scalar(self, op, allow_empty)
 
-        op = _op.get_typed_op(op if op is not None else _op.monoid.plus, self.dtype, kind="monoid")
-        return ScalarExpression("reduce", "GrB_Vector_reduce_Monoid_Scalar", [self], op=op,
-                                allow_empty=allow_empty)
+    def apply(self, op, right=None, *, left=None):
+        return _apply_expr(self, op, right, left)
 
     def isequal(self, other, *, check_dtype=False):
         if not isinstance(other, Vector):

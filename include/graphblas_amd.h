@@ -88,6 +88,7 @@ typedef enum { GrB_CSR_FORMAT = 0, GrB_CSC_FORMAT = 1, GrB_COO_FORMAT = 2 } GrB_
 
 typedef struct GB_Type_opaque *GrB_Type;
 typedef struct GB_BinaryOp_opaque *GrB_BinaryOp;
+typedef struct GB_UnaryOp_opaque *GrB_UnaryOp;
 typedef struct GB_Monoid_opaque *GrB_Monoid;
 typedef struct GB_Semiring_opaque *GrB_Semiring;
 typedef struct GB_Descriptor_opaque *GrB_Descriptor;
@@ -123,6 +124,11 @@ GrB_Info GrB_Type_free(GrB_Type *type);
 GrB_Info GrB_BinaryOp_free(GrB_BinaryOp *op);
 GrB_Info GrB_Monoid_free(GrB_Monoid *monoid);
 GrB_Info GrB_Semiring_free(GrB_Semiring *semiring);
+GrB_Info GrB_UnaryOp_free(GrB_UnaryOp *op);
+/* semiring from a builtin monoid and a builtin binary operator whose output type is the
+ * monoid's (python-graphblas registers e.g. plus_pow this way for agg.sum_of_squares,
+ * reference core/operator/agg.py:271-276) */
+GrB_Info GrB_Semiring_new(GrB_Semiring *semiring, GrB_Monoid add, GrB_BinaryOp multiply);
 GrB_Info GxB_Semiring_add(GrB_Monoid *add, GrB_Semiring semiring);
 GrB_Info GxB_Semiring_multiply(GrB_BinaryOp *multiply, GrB_Semiring semiring);
 
@@ -169,7 +175,15 @@ GrB_Info GrB_Matrix_exportHint(GrB_Format *format, GrB_Matrix A);
     GrB_Info GrB_Matrix_reduce_##T(ctype *c, const GrB_BinaryOp accum, const GrB_Monoid monoid, \
                                    const GrB_Matrix A, const GrB_Descriptor desc);              \
     GrB_Info GxB_Matrix_build_Scalar_##T(GrB_Matrix C, const GrB_Index *I, const GrB_Index *J,  \
-                                         ctype x, GrB_Index nvals);
+                                         ctype x, GrB_Index nvals);                              \
+    GrB_Info GrB_Matrix_apply_BinaryOp1st_##T(GrB_Matrix C, const GrB_Matrix Mask,              \
+                                              const GrB_BinaryOp accum, const GrB_BinaryOp op,  \
+                                              ctype x, const GrB_Matrix A,                      \
+                                              const GrB_Descriptor desc);                       \
+    GrB_Info GrB_Matrix_apply_BinaryOp2nd_##T(GrB_Matrix C, const GrB_Matrix Mask,              \
+                                              const GrB_BinaryOp accum, const GrB_BinaryOp op,  \
+                                              const GrB_Matrix A, ctype y,                      \
+                                              const GrB_Descriptor desc);
 
 #define GB_DECLARE_TYPED_VECTOR(T, ctype)                                                          \
     GrB_Info GrB_Vector_build_##T(GrB_Vector w, const GrB_Index *I, const ctype *X,             \
@@ -186,7 +200,15 @@ GrB_Info GrB_Matrix_exportHint(GrB_Format *format, GrB_Matrix A);
     GrB_Info GrB_Scalar_setElement_##T(GrB_Scalar s, ctype x);                                   \
     GrB_Info GrB_Scalar_extractElement_##T(ctype *x, const GrB_Scalar s);                        \
     GrB_Info GxB_Vector_build_Scalar_##T(GrB_Vector w, const GrB_Index *I, ctype x,             \
-                                         GrB_Index nvals);
+                                         GrB_Index nvals);                                      \
+    GrB_Info GrB_Vector_apply_BinaryOp1st_##T(GrB_Vector w, const GrB_Vector mask,              \
+                                              const GrB_BinaryOp accum, const GrB_BinaryOp op,  \
+                                              ctype x, const GrB_Vector u,                      \
+                                              const GrB_Descriptor desc);                       \
+    GrB_Info GrB_Vector_apply_BinaryOp2nd_##T(GrB_Vector w, const GrB_Vector mask,              \
+                                              const GrB_BinaryOp accum, const GrB_BinaryOp op,  \
+                                              const GrB_Vector u, ctype y,                      \
+                                              const GrB_Descriptor desc);
 
 #define GB_FOR_EACH_TYPE(X)                                                                        \
     X(BOOL, bool)                                                                                  \
@@ -269,6 +291,22 @@ GrB_Info GrB_Matrix_reduce_Monoid_Scalar(GrB_Scalar s, const GrB_BinaryOp accum,
 GrB_Info GrB_Vector_reduce_Monoid_Scalar(GrB_Scalar s, const GrB_BinaryOp accum,
                                          const GrB_Monoid monoid, const GrB_Vector u,
                                          const GrB_Descriptor desc);
+/* w<mask> = accum(w, reduce each row of A' with the monoid): lowered to a semiring SpMV
+ * (monoid, FIRST) against an iso-full vector, the reference's own lowering of reductions
+ * (core/operator/agg.py:207-279); A' = A^T (desc INP0 = TRAN) reduces columns
+ * (core/matrix.py:2583,2620). */
+GrB_Info GrB_Matrix_reduce_Monoid(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum,
+                                  const GrB_Monoid monoid, const GrB_Matrix A,
+                                  const GrB_Descriptor desc);
+GrB_Info GrB_Matrix_reduce_BinaryOp(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum,
+                                    const GrB_BinaryOp op, const GrB_Matrix A,
+                                    const GrB_Descriptor desc);
+/* apply (reference core/vector.py:1370,1404,1447; core/matrix.py:2356,2390,2433): values map,
+ * structure kept; iso inputs stay iso (one value computed). */
+GrB_Info GrB_Vector_apply(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum,
+                          const GrB_UnaryOp op, const GrB_Vector u, const GrB_Descriptor desc);
+GrB_Info GrB_Matrix_apply(GrB_Matrix C, const GrB_Matrix Mask, const GrB_BinaryOp accum,
+                          const GrB_UnaryOp op, const GrB_Matrix A, const GrB_Descriptor desc);
 GrB_Info GrB_transpose(GrB_Matrix C, const GrB_Matrix Mask, const GrB_BinaryOp accum,
                        const GrB_Matrix A, const GrB_Descriptor desc);
 

@@ -51,6 +51,12 @@ OPCODE = {n: i for i, n in enumerate(BINOPS)}
 BOOL_OUT = {"EQ", "NE", "GT", "LT", "GE", "LE"}
 POSITIONAL = {"FIRSTI", "FIRSTI1", "FIRSTJ", "FIRSTJ1", "SECONDI", "SECONDI1", "SECONDJ", "SECONDJ1"}
 
+# unary operators (reference core/operator/unary.py:289-340 name patterns)
+UNOPS = ["IDENTITY", "AINV", "MINV", "ABS", "LNOT", "ONE", "BNOT",
+         "SQRT", "LOG", "LOG2", "LOG10", "EXP", "EXP2", "FLOOR", "CEIL", "ROUND", "TRUNC",
+         "SIN", "COS", "TAN"]
+UCODE = {n: i for i, n in enumerate(UNOPS)}
+
 MONOIDS = ["PLUS", "TIMES", "MIN", "MAX", "ANY", "LOR", "LAND", "LXOR", "LXNOR",
            "BOR", "BAND", "BXOR", "BXNOR"]
 MCODE = {n: i for i, n in enumerate(MONOIDS)}
@@ -122,6 +128,26 @@ def binop_table():
     for op in sorted(POSITIONAL):
         for t in ["INT32", "INT64"]:
             add(f"GxB_{op}_{t}", op, None, t)
+    return out
+
+
+def unop_table():
+    """-> list of (name, opcode name, type)."""
+    out = []
+    for op in ["IDENTITY", "AINV", "MINV", "ABS"]:
+        for t in TYPES:
+            out.append((f"GrB_{op}_{t[0]}", op, t[0]))
+    out.append(("GrB_LNOT", "LNOT", "BOOL"))
+    for t in TYPES[1:]:
+        out.append((f"GxB_LNOT_{t[0]}", "LNOT", t[0]))
+    for t in TYPES:
+        out.append((f"GxB_ONE_{t[0]}", "ONE", t[0]))
+    for t in INTS:
+        out.append((f"GrB_BNOT_{t}", "BNOT", t))
+    for op in ["SQRT", "LOG", "LOG2", "LOG10", "EXP", "EXP2", "FLOOR", "CEIL", "ROUND", "TRUNC",
+               "SIN", "COS", "TAN"]:
+        for t in ["FP32", "FP64"]:
+            out.append((f"GxB_{op}_{t}", op, t))
     return out
 
 
@@ -203,6 +229,7 @@ HEADER_NOTE = "/* GENERATED by tools/gen_builtins.py -- do not edit. */\n"
 
 def main():
     binops = binop_table()
+    unops = unop_table()
     monoids = monoid_table()
     semirings = semiring_table(binops, monoids)
     bmap = {b[0]: b for b in binops}
@@ -217,6 +244,10 @@ def main():
     for i, n in enumerate(BINOPS):
         lines.append(f"    GBAMD_OP_{n} = {i},\n")
     lines.append(f"    GBAMD_OP_COUNT = {len(BINOPS)}\n}};\n")
+    lines.append("/* unary operator codes */\nenum gbamd_unop_code {\n")
+    for i, n in enumerate(UNOPS):
+        lines.append(f"    GBAMD_UOP_{n} = {i},\n")
+    lines.append(f"    GBAMD_UOP_COUNT = {len(UNOPS)}\n}};\n")
     lines.append("/* monoid codes */\nenum gbamd_monoid_code {\n")
     for i, n in enumerate(MONOIDS):
         lines.append(f"    GBAMD_MON_{n} = {i},\n")
@@ -233,6 +264,9 @@ def main():
     d.append("/* builtin binary operators (reference core/operator/binary.py:332-369) */\n")
     for b in binops:
         d.append(f"GB_EXTERN GrB_BinaryOp {b[0]};\n")
+    d.append("/* builtin unary operators (reference core/operator/unary.py) */\n")
+    for u in unops:
+        d.append(f"GB_EXTERN GrB_UnaryOp {u[0]};\n")
     d.append("/* builtin monoids (reference core/operator/monoid.py:179-195) */\n")
     for m in monoids:
         d.append(f"GB_EXTERN GrB_Monoid {m[0]};\n")
@@ -256,6 +290,8 @@ def main():
     for b in binops:
         x = f"&T_{b[2]}" if b[2] else "nullptr"
         c.append(f"GB_BinaryOp_opaque B_{b[0]} = {{GB_MAGIC, GBAMD_OP_{b[1]}, {x}, {x}, &T_{b[3]}, \"{b[0]}\"}};\n")
+    for u in unops:
+        c.append(f"GB_UnaryOp_opaque U_{u[0]} = {{GB_MAGIC, GBAMD_UOP_{u[1]}, &T_{u[2]}, &T_{u[2]}, \"{u[0]}\"}};\n")
     for m in monoids:
         c.append(f"GB_Monoid_opaque M_{m[0]} = {{GB_MAGIC, GBAMD_MON_{m[1]}, &T_{m[2]}, &B_{m[3]}, \"{m[0]}\"}};\n")
     for s in semirings:
@@ -270,6 +306,8 @@ def main():
         c.append(f"GrB_Type GrB_{t[0]} = &T_{t[0]};\n")
     for b in binops:
         c.append(f"GrB_BinaryOp {b[0]} = &B_{b[0]};\n")
+    for u in unops:
+        c.append(f"GrB_UnaryOp {u[0]} = &U_{u[0]};\n")
     for m in monoids:
         c.append(f"GrB_Monoid {m[0]} = &M_{m[0]};\n")
     for s in semirings:
@@ -293,6 +331,8 @@ def main():
             c.append(f"    {{\"{a}\", 3, (void*)&S_{s[0]}}},\n")
     for name in DESCS.values():
         c.append(f"    {{\"{name}\", 4, (void*)&D_{name}}},\n")
+    for u in unops:
+        c.append(f"    {{\"{u[0]}\", 5, (void*)&U_{u[0]}}},\n")
     c.append("    {nullptr, -1, nullptr}\n};\n")
     with open(os.path.join(ROOT, "graph-python_amd", "csrc", "gb_builtins.cpp"), "w") as f:
         f.write("".join(c))
@@ -303,9 +343,13 @@ def main():
     p.append("TYPES = " + repr([(t[0], t[2]) for t in TYPES]) + "\n\n")
     p.append("BINOP_CODES = " + repr(BINOPS) + "\n\n")
     p.append("MONOID_CODES = " + repr(MONOIDS) + "\n\n")
+    p.append("UNOP_CODES = " + repr(UNOPS) + "\n\n")
     p.append("# name: (opcode name, xtype or None for positional, ztype)\nBINOPS = {\n")
     for b in binops:
         p.append(f"    {b[0]!r}: ({b[1]!r}, {b[2]!r}, {b[3]!r}),\n")
+    p.append("}\n\n# name: (opcode name, type)\nUNOPS = {\n")
+    for u in unops:
+        p.append(f"    {u[0]!r}: ({u[1]!r}, {u[2]!r}),\n")
     p.append("}\n\n# name: (monoid code name, type, binop name)\nMONOIDS = {\n")
     for m in monoids:
         p.append(f"    {m[0]!r}: ({m[1]!r}, {m[2]!r}, {m[3]!r}),\n")
@@ -318,7 +362,7 @@ def main():
     p.append("}\n")
     with open(os.path.join(ROOT, "graph-python_amd", "graphblas_amd", "_builtins.py"), "w") as f:
         f.write("".join(p))
-    print(f"types={len(TYPES)} binops={len(binops)} monoids={len(monoids)} "
+    print(f"types={len(TYPES)} binops={len(binops)} unops={len(unops)} monoids={len(monoids)} "
           f"semirings={len(semirings)} (+{sum(len(s[3]) for s in semirings)} aliases) "
           f"descriptors={len(DESCS)}")
 
