@@ -4,7 +4,7 @@
 // Most hot-path calls never launch a merge: with no accumulator and either no
 // mask or a mask the kernel already applied under `replace` (BFS:
 // q<!v.S, replace> = ...), T simply becomes C's new storage.  Otherwise a
-// word-parallel (vectors) or row-parallel (matrices) merge runs.
+// word-parallel (vectors) or entry-parallel (matrices) merge runs.
 //
 // Mixed-type accumulators (accum type != C type) are evaluated by casting C
 // and T into the accumulator type, merging there and casting back; entries
@@ -268,56 +268,120 @@ bool gb_writeback_vector(GB_Obj *C, gb_vec_result &T, GB_Obj *M, const gb_desc &
 }
 
 // ================================================================== matrices
-template <class CT, bool FILL>
-__global__ __launch_bounds__(WB_BLOCK) void k_mat_merge(
-    int64_t nrows, const int64_t *__restrict__ crp, const int32_t *__restrict__ cci, const CT *__restrict__ cvx,
-    bool c_iso, const int64_t *__restrict__ trp, const int32_t *__restrict__ tci, const CT *__restrict__ tvx,
-    bool t_iso, const int64_t *__restrict__ mrp, const int32_t *__restrict__ mci, bool has_mask, bool mcomp,
-    bool replace, int accum, int64_t *__restrict__ orp, int32_t *__restrict__ oci, CT *__restrict__ ovx) {
-    WB_STRIDE(i, nrows) {
-        int64_t pc = crp[i], ec = crp[i + 1], pt = trp[i], et = trp[i + 1];
-        int64_t pm = has_mask ? mrp[i] : 0, em = has_mask ? mrp[i + 1] : 0;
-        int64_t o = FILL ? orp[i] : 0;
-        while (pc < ec || pt < et) {
-            int32_t jc = pc < ec ? cci[pc] : INT32_MAX;
-            int32_t jt = pt < et ? tci[pt] : INT32_MAX;
-            int32_t j = jc < jt ? jc : jt;
-            bool c = jc == j, t = jt == j;
-            bool m;
-            if (has_mask) {
-                while (pm < em && mci[pm] < j) pm++;
-                m = (pm < em && mci[pm] == j) != mcomp;
+// Entry-parallel merge of C and T under the mask (one thread per stored entry,
+// so R-MAT hub rows with 10^4-10^5 entries do not serialise a thread):
+//   1. flag every entry of C and of T that survives (k_merge_flag_c / _t);
+//   2. exclusive scans of both flag arrays (sc, st);
+//   3. row r of the output starts at sc[crp[r]] + st[trp[r]];
+//   4. a surviving C entry (r, j) lands at sc[e] + st[lower_bound of j in T's row r],
+//      a surviving T entry at st[e] + sc[lower_bound of j in C's row r]
+//      (both rows sorted, so this is their merge order).
+// A C entry survives where the mask is false (unless replace) or where it is true,
+// accum is set and T has no entry; a T entry survives where the mask is true and
+// carries accum(C, T) when C has the entry too.
+__device__ __forceinline__ int64_t wb_row_of(const int64_t *__restrict__ rp, int64_t nrows, int64_t e) {
+    int64_t lo = 0, hi = nrows;  // last r with rp[r] <= e
+    while (hi - lo > 1) {
+        int64_t mid = (lo + hi) >> 1;
+        if (rp[mid] <= e) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ int64_t wb_lower_bound(const int32_t *__restrict__ ci, int64_t lo, int64_t hi, int32_t j) {
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (ci[mid] < j) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ bool wb_mask_at(const int64_t *__restrict__ mrp, const int32_t *__restrict__ mci,
+                                          bool has_mask, bool mcomp, int64_t r, int32_t j) {
+    if (!has_mask) return !mcomp;
+    int64_t a = mrp[r], b = mrp[r + 1];
+    int64_t p = wb_lower_bound(mci, a, b, j);
+    return (p < b && mci[p] == j) != mcomp;
+}
+
+__global__ __launch_bounds__(WB_BLOCK) void k_merge_flag_c(
+    int64_t nrows, int64_t cnz, const int64_t *__restrict__ crp, const int32_t *__restrict__ cci,
+    const int64_t *__restrict__ trp, const int32_t *__restrict__ tci, const int64_t *__restrict__ mrp,
+    const int32_t *__restrict__ mci, bool has_mask, bool mcomp, bool replace, bool accum,
+    int64_t *__restrict__ flag) {
+    WB_STRIDE(e, cnz) {
+        const int64_t r = wb_row_of(crp, nrows, e);
+        const int32_t j = cci[e];
+        bool keep;
+        if (wb_mask_at(mrp, mci, has_mask, mcomp, r, j)) {
+            if (accum) {
+                int64_t a = trp[r], b = trp[r + 1];
+                int64_t p = wb_lower_bound(tci, a, b, j);
+                keep = !(p < b && tci[p] == j);
             } else {
-                m = !mcomp;
+                keep = false;
             }
-            bool have = false;
-            CT v = CT();
-            if (m) {
-                if (accum >= 0 && c && t) {
-                    if (FILL) v = gb_binop<CT>(accum, cvx[c_iso ? 0 : pc], tvx[t_iso ? 0 : pt]);
-                    have = true;
-                } else if (t) {
-                    if (FILL) v = tvx[t_iso ? 0 : pt];
-                    have = true;
-                } else if (accum >= 0 && c) {
-                    if (FILL) v = cvx[c_iso ? 0 : pc];
-                    have = true;
-                }
-            } else if (!replace && c) {
-                if (FILL) v = cvx[c_iso ? 0 : pc];
-                have = true;
-            }
-            if (have) {
-                if (FILL) {
-                    oci[o] = j;
-                    ovx[o] = v;
-                }
-                o++;
-            }
-            if (c) pc++;
-            if (t) pt++;
+        } else {
+            keep = !replace;
         }
-        if (!FILL) orp[i] = o;
+        flag[e] = keep;
+    }
+}
+
+__global__ __launch_bounds__(WB_BLOCK) void k_merge_flag_t(
+    int64_t nrows, int64_t tnz, const int64_t *__restrict__ trp, const int32_t *__restrict__ tci,
+    const int64_t *__restrict__ mrp, const int32_t *__restrict__ mci, bool has_mask, bool mcomp, bool within_mask,
+    int64_t *__restrict__ flag) {
+    WB_STRIDE(e, tnz) {
+        bool keep = true;
+        if (!within_mask) {
+            const int64_t r = wb_row_of(trp, nrows, e);
+            keep = wb_mask_at(mrp, mci, has_mask, mcomp, r, tci[e]);
+        }
+        flag[e] = keep;
+    }
+}
+
+__global__ void k_merge_rowptr(int64_t nrows, const int64_t *__restrict__ crp, const int64_t *__restrict__ trp,
+                               const int64_t *__restrict__ sc, const int64_t *__restrict__ st,
+                               int64_t *__restrict__ orp) {
+    WB_STRIDE(r, nrows + 1) orp[r] = sc[crp[r]] + st[trp[r]];
+}
+
+template <class CT>
+__global__ __launch_bounds__(WB_BLOCK) void k_merge_place_c(
+    int64_t nrows, int64_t cnz, const int64_t *__restrict__ crp, const int32_t *__restrict__ cci,
+    const CT *__restrict__ cvx, bool c_iso, const int64_t *__restrict__ trp, const int32_t *__restrict__ tci,
+    const int64_t *__restrict__ sc, const int64_t *__restrict__ st, int32_t *__restrict__ oci,
+    CT *__restrict__ ovx) {
+    WB_STRIDE(e, cnz) {
+        if (sc[e + 1] == sc[e]) continue;
+        const int64_t r = wb_row_of(crp, nrows, e);
+        const int32_t j = cci[e];
+        const int64_t p = wb_lower_bound(tci, trp[r], trp[r + 1], j);
+        const int64_t o = sc[e] + st[p];
+        oci[o] = j;
+        ovx[o] = cvx[c_iso ? 0 : e];
+    }
+}
+
+template <class CT>
+__global__ __launch_bounds__(WB_BLOCK) void k_merge_place_t(
+    int64_t nrows, int64_t tnz, const int64_t *__restrict__ trp, const int32_t *__restrict__ tci,
+    const CT *__restrict__ tvx, bool t_iso, const int64_t *__restrict__ crp, const int32_t *__restrict__ cci,
+    const CT *__restrict__ cvx, bool c_iso, int accum, const int64_t *__restrict__ sc,
+    const int64_t *__restrict__ st, int32_t *__restrict__ oci, CT *__restrict__ ovx) {
+    WB_STRIDE(e, tnz) {
+        if (st[e + 1] == st[e]) continue;
+        const int64_t r = wb_row_of(trp, nrows, e);
+        const int32_t j = tci[e];
+        const int64_t a = crp[r], b = crp[r + 1];
+        const int64_t p = wb_lower_bound(cci, a, b, j);
+        CT v = tvx[t_iso ? 0 : e];
+        if (accum >= 0 && p < b && cci[p] == j) v = gb_binop<CT>(accum, cvx[c_iso ? 0 : p], v);
+        const int64_t o = st[e] + sc[p];
+        oci[o] = j;
+        ovx[o] = v;
     }
 }
 
@@ -362,29 +426,40 @@ void gb_writeback_matrix(GB_Obj *C, gb_mat_result &T, GB_Obj *M, const gb_desc &
     gb_scratch s;
     const void *cvals = (wcode != ct) ? gb_view_vals_as(cv, wcode, s) : cv.vals;
     cast_mat_result(T, wcode);
-    int64_t *cnt = s.get<int64_t>(nrows + 1);
-    int64_t *orp = gb_malloc_n<int64_t>(nrows + 1);
-    bool has_mask = mask.present;
-    gb_with_type(wcode, [&](auto z) {
-        using W = decltype(z);
-        if (nrows)
-            hipLaunchKernelGGL((k_mat_merge<W, false>), dim3(wb_grid(nrows)), dim3(WB_BLOCK), 0, gb_stream(), nrows,
-                               cv.rowptr, cv.colidx, (const W *)cvals, cv.iso, T.rowptr, T.colidx, (const W *)T.vals,
-                               T.iso, mask.rowptr, mask.colidx, has_mask, mask.comp, d.replace,
-                               accum ? accum->opcode : -1, cnt, nullptr, nullptr);
-    });
+    const bool has_mask = mask.present;
+    const int64_t cnz = cv.nvals, tnz = T.nvals;
+    int64_t *fc = s.get<int64_t>(std::max<int64_t>(cnz, 1));
+    int64_t *ft = s.get<int64_t>(std::max<int64_t>(tnz, 1));
+    int64_t *sc = s.get<int64_t>(cnz + 1);
+    int64_t *st = s.get<int64_t>(tnz + 1);
+    if (cnz)
+        hipLaunchKernelGGL(k_merge_flag_c, dim3(wb_grid(cnz)), dim3(WB_BLOCK), 0, gb_stream(), nrows, cnz, cv.rowptr,
+                           cv.colidx, T.rowptr, T.colidx, mask.rowptr, mask.colidx, has_mask, mask.comp, d.replace,
+                           accum != nullptr, fc);
+    if (tnz)
+        hipLaunchKernelGGL(k_merge_flag_t, dim3(wb_grid(tnz)), dim3(WB_BLOCK), 0, gb_stream(), nrows, tnz, T.rowptr,
+                           T.colidx, mask.rowptr, mask.colidx, has_mask, mask.comp,
+                           T.within_mask && has_mask && !mask.comp, ft);
     GB_LAUNCH_CHECK();
-    gb_exclusive_scan_i64(cnt, orp, nrows);
+    gb_exclusive_scan_i64(fc, sc, cnz);
+    gb_exclusive_scan_i64(ft, st, tnz);
+    int64_t *orp = gb_malloc_n<int64_t>(nrows + 1);
+    hipLaunchKernelGGL(k_merge_rowptr, dim3(wb_grid(nrows + 1)), dim3(WB_BLOCK), 0, gb_stream(), nrows, cv.rowptr,
+                       T.rowptr, sc, st, orp);
+    GB_LAUNCH_CHECK();
     int64_t nz = gb_read_i64(orp + nrows);
-    int32_t *oci = gb_malloc_n<int32_t>(nz);
-    void *ovx = gb_malloc(nz * gb_type_size(wcode));
+    int32_t *oci = gb_malloc_n<int32_t>(std::max<int64_t>(nz, 1));
+    void *ovx = gb_malloc(std::max<int64_t>(nz, 1) * gb_type_size(wcode));
     gb_with_type(wcode, [&](auto z) {
         using W = decltype(z);
-        if (nrows)
-            hipLaunchKernelGGL((k_mat_merge<W, true>), dim3(wb_grid(nrows)), dim3(WB_BLOCK), 0, gb_stream(), nrows,
-                               cv.rowptr, cv.colidx, (const W *)cvals, cv.iso, T.rowptr, T.colidx, (const W *)T.vals,
-                               T.iso, mask.rowptr, mask.colidx, has_mask, mask.comp, d.replace,
-                               accum ? accum->opcode : -1, orp, oci, (W *)ovx);
+        if (cnz)
+            hipLaunchKernelGGL((k_merge_place_c<W>), dim3(wb_grid(cnz)), dim3(WB_BLOCK), 0, gb_stream(), nrows, cnz,
+                               cv.rowptr, cv.colidx, (const W *)cvals, cv.iso, T.rowptr, T.colidx, sc, st, oci,
+                               (W *)ovx);
+        if (tnz)
+            hipLaunchKernelGGL((k_merge_place_t<W>), dim3(wb_grid(tnz)), dim3(WB_BLOCK), 0, gb_stream(), nrows, tnz,
+                               T.rowptr, T.colidx, (const W *)T.vals, T.iso, cv.rowptr, cv.colidx, (const W *)cvals,
+                               cv.iso, accum ? accum->opcode : -1, sc, st, oci, (W *)ovx);
     });
     GB_LAUNCH_CHECK();
     gb_free(T.rowptr);

@@ -350,14 +350,16 @@ SEMIRINGS = [
 
 
 @pytest.mark.parametrize("name,mon,mul,dt", SEMIRINGS)
-@pytest.mark.parametrize("masked", ["none", "struct", "comp_replace", "value"])
+@pytest.mark.parametrize("masked", ["none", "struct", "comp_replace", "value", "struct_accum", "value_keep",
+                                    "comp_accum"])
 def test_random_mxm_vs_oracle(gb, name, mon, mul, dt, masked):
     rng = np.random.default_rng(hash((name, dt, masked)) % 2**32)
     n, k, m = 37, 53, 41
     Ao = _rand_csr(rng, n, k, 0.15, dt)
     Bo = _rand_csr(rng, k, m, 0.15, dt)
     Mo = _rand_csr(rng, n, m, 0.3, "BOOL")
-    Co = _rand_csr(rng, n, m, 0.1, dt) if masked == "comp_replace" else O.Csr.empty(n, m, dt)
+    nonempty = masked in ("comp_replace", "struct_accum", "value_keep", "comp_accum")
+    Co = _rand_csr(rng, n, m, 0.25, dt) if nonempty else O.Csr.empty(n, m, dt)
     sr = getattr(gb.semiring, name)[dt]
     Ag, Bg, Mg = _to_gb(gb, Ao), _to_gb(gb, Bo), _to_gb(gb, Mo)
     Cg = _to_gb(gb, Co)
@@ -370,6 +372,16 @@ def test_random_mxm_vs_oracle(gb, name, mon, mul, dt, masked):
     elif masked == "comp_replace":
         Cg(~Mg.S, replace=True) << Ag.mxm(Bg, sr)
         kw = dict(mask=Mo, mask_struct=True, mask_comp=True, replace=True)
+    elif masked == "struct_accum":
+        # merge into a non-empty C: entries outside the mask kept, accum where both exist
+        Cg(Mg.S, gb.binary.max) << Ag.mxm(Bg, sr)
+        kw = dict(mask=Mo, mask_struct=True, accum=("MAX", dt))
+    elif masked == "value_keep":
+        Cg(Mg.V) << Ag.mxm(Bg, sr)
+        kw = dict(mask=Mo)
+    elif masked == "comp_accum":
+        Cg(~Mg.S, gb.binary.plus) << Ag.mxm(Bg, sr)
+        kw = dict(mask=Mo, mask_struct=True, mask_comp=True, accum=("PLUS", dt))
     else:
         Cg(Mg.V) << Ag.mxm(Bg, sr)
         kw = dict(mask=Mo)
