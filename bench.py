@@ -58,6 +58,7 @@ def parse():
     # rehearsal of the N>1 path on one GPU: all ranks on one device, gloo transport
     p.add_argument("--dist-backend", default="nccl")
     p.add_argument("--device", type=int, default=None, help="override LOCAL_RANK's device")
+    p.add_argument("--knob", action="append", default=[], help="library knob key=value (ablations)")
     return p.parse_args()
 
 
@@ -241,6 +242,9 @@ def main():
     import oracle as O
 
     lib = gb.lib
+    for kv in args.knob:
+        k, v = kv.split("=")
+        gb.set_knob(k, int(v))
     ok(lib.GxB_Context_set_device(local_rank), "set_device")
     stream = torch.cuda.Stream()
     gb.set_stream(stream)

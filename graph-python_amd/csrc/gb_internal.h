@@ -6,6 +6,8 @@
 // Scalar._as_vector core/scalar.py:555-573) are legal: the operation looks at
 // the object's kind and converts storage on the fly.
 #pragma once
+#include <atomic>
+#include <utility>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -131,9 +133,15 @@ void gb_hip_check(hipError_t e, const char *what);
 // API-boundary wrapper: runs body, converts exceptions to GrB_Info and stores
 // the message on the error object (reference core/exceptions.py:124-155 reads
 // it back with GrB_<Type>_error on the call's output argument).
-template <class F>
-GrB_Info gb_api(GB_Obj *errobj, F &&body) {
+// a deferred assign (gb_asg, gb_ops.hip) is carried out before any API call
+// other than the SpMV that may fuse it
+extern std::atomic<bool> g_pending_active;
+void gb_pending_flush();
+
+template <bool FLUSH = true, class F>
+GrB_Info gb_api_impl(GB_Obj *errobj, F &&body) {
     try {
+        if (FLUSH && g_pending_active.load(std::memory_order_acquire)) gb_pending_flush();
         body();
         if (errobj && errobj->magic == GB_MAGIC) errobj->err.clear();
         return GrB_SUCCESS;
@@ -146,6 +154,15 @@ GrB_Info gb_api(GB_Obj *errobj, F &&body) {
     } catch (...) {
         return GrB_PANIC;
     }
+}
+template <class F>
+GrB_Info gb_api(GB_Obj *errobj, F &&body) {
+    return gb_api_impl<true>(errobj, std::forward<F>(body));
+}
+// GrB_mxv / GrB_vxm: the deferred assign is fused or flushed inside (do_spmv)
+template <class F>
+GrB_Info gb_api_keep_pending(GB_Obj *errobj, F &&body) {
+    return gb_api_impl<false>(errobj, std::forward<F>(body));
 }
 
 // ------------------------------------------------------------------ context
@@ -349,8 +366,22 @@ void gb_writeback_matrix(GB_Obj *C, gb_mat_result &T, GB_Obj *M, const gb_desc &
 // kernels of the hot path (gb_mxv.hip, gb_mxm.hip)
 // A: rows = output positions (pull); Apush: the other orientation (rows = u's
 // positions) or nullptr; the device picks push or pull per call.
+// A deferred `w<q>(:) = x` (GrB_Vector_assign with a value or structural mask q,
+// no accum / replace, all indices) carried out by the iso SpMV kernel whose input
+// is q and whose mask is w's structure (the BFS level loop: v<q> = d;
+// q<!v.S> = q lor.land A).  gb_ops.hip defers such assigns; every other API call
+// performs them first (gb_pending_flush, called by gb_api).
+struct gb_asg {
+    uint64_t *bits = nullptr;  // w's bitmap (read as the call's mask, OR q)
+    void *vals = nullptr;      // w's dense values
+    int size = 0;              // value size in bytes
+    unsigned long long x = 0;  // the value's bytes
+    const void *q_iso = nullptr;  // q's iso value when q is a value mask (nullptr: structure)
+    int q_iso_code = -1;
+    int64_t *count = nullptr;  // w's device count
+};
 void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, gb_bitmap_view &u,
-             const gb_vmask &mask, GrB_Semiring sr, bool flip);
+             const gb_vmask &mask, GrB_Semiring sr, bool flip, const gb_asg *asg = nullptr);
 bool gb_spmv_result_iso(GrB_Semiring sr, bool a_iso, bool u_iso, bool flip);
 void gb_spgemm(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, gb_csr_view *BT,
                gb_mmask &mask, GrB_Semiring sr);

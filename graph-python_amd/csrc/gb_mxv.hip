@@ -120,6 +120,7 @@ enum { ST_PUSH = 0 };
 
 struct gb_dir_rule {
     const int64_t *mask_count;  // device count of set mask bits (nullptr: unknown)
+    const int64_t *extra_count; // entries a fused assign adds to the mask (upper bound; nullptr: none)
     bool mcomp;
     int64_t n_out, nnz, alpha;
     int force_push;
@@ -130,7 +131,9 @@ struct gb_dir_rule {
 __device__ __forceinline__ bool gb_dir_decide(long long mf, const gb_dir_rule &rule) {
     int64_t open = rule.n_out;  // rows the pull kernel would visit
     if (rule.mask_count) {
-        const int64_t mc = *rule.mask_count;
+        int64_t mc = *rule.mask_count;
+        if (rule.extra_count) mc += *rule.extra_count;
+        if (mc > rule.n_out) mc = rule.n_out;
         open = rule.mcomp ? (rule.n_out - mc) : mc;
     }
     const double avg = rule.n_out ? (double)rule.nnz / (double)rule.n_out : 0.0;
@@ -194,11 +197,12 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_dir_prep(
 __device__ __forceinline__ long long gb_push_targets(const int32_t (&j)[4], bool (&ok)[4],
                                                      const uint64_t *__restrict__ mbits, bool mcomp,
                                                      unsigned long long *__restrict__ tbits,
-                                                     const int64_t *__restrict__ hprow, long long &mfn) {
+                                                     const int64_t *__restrict__ hprow, long long &mfn,
+                                                     const uint64_t *__restrict__ qbits) {
     if (mbits) {
 #pragma unroll
         for (int u = 0; u < 4; u++)
-            if (ok[u]) ok[u] = gb_bit(mbits, j[u]) != mcomp;
+            if (ok[u]) ok[u] = (gb_bit(mbits, j[u]) || (qbits && gb_bit(qbits, j[u]))) != mcomp;
     }
     unsigned long long cur[4];
 #pragma unroll
@@ -282,6 +286,40 @@ __device__ __forceinline__ int gb_wlist_find(const gb_wlist &L, int n, int e) {
     return lo;
 }
 
+// The fused assign (gb_asg) for the 4 words w0..w0+3 of q (lanes 0-3 hold word
+// w0 + (lane & 3) in qw): w's presence words |= q, w's value at each q bit = x
+// (one lane per position: coalesced stores); returns the entries added to w.
+struct gb_asg_dev {
+    uint64_t *bits;
+    void *vals;
+    int size;
+    unsigned long long x;
+};
+__device__ __forceinline__ void gb_store_sized(void *base, int64_t i, int size, unsigned long long x) {
+    switch (size) {
+    case 1: ((uint8_t *)base)[i] = (uint8_t)x; break;
+    case 2: ((uint16_t *)base)[i] = (uint16_t)x; break;
+    case 4: ((uint32_t *)base)[i] = (uint32_t)x; break;
+    default: ((unsigned long long *)base)[i] = x; break;
+    }
+}
+__device__ __forceinline__ long long gb_asg_words(const gb_asg_dev &g, int64_t w0, int64_t nwords, uint64_t qw,
+                                                 int lane) {
+    long long added = 0;
+    const int64_t wl = w0 + (lane & 3);
+    if (lane < 4 && wl < nwords && qw) {
+        const uint64_t c = g.bits[wl], nwd = c | qw;
+        if (nwd != c) g.bits[wl] = nwd;
+        added = (long long)__popcll(nwd) - (long long)__popcll(c);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const uint64_t word = __shfl(qw, u, 64);
+        if ((word >> lane) & 1ULL) gb_store_sized(g.vals, ((w0 + u) << 6) + lane, g.size, g.x);
+    }
+    return added;
+}
+
 // Push (top-down).  First the matrix's hub chunks (rows longer than H cut into
 // H-edge pieces, a static table; a wave tests 16 strided entries against the
 // frontier at once and expands the hits, 256 edges a step).  Then the frontier
@@ -292,7 +330,9 @@ __device__ __forceinline__ long long gb_push_phase(int64_t nwords_u, const uint6
                                                   const int32_t *__restrict__ hubs, int64_t nhubs, int64_t H,
                                                   const uint64_t *__restrict__ mbits, bool mcomp,
                                                   unsigned long long *__restrict__ tbits, gb_wlist &L,
-                                                  const int64_t *__restrict__ hprow, long long &mfn) {
+                                                  const int64_t *__restrict__ hprow, long long &mfn,
+                                                  const uint64_t *__restrict__ qbits, const gb_asg_dev &g,
+                                                  long long &adelta) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -325,7 +365,7 @@ __device__ __forceinline__ long long gb_push_phase(int64_t nwords_u, const uint6
                     ok[u] = p + 64 * u < p1;
                     j[u] = ok[u] ? pcol[p + 64 * u] : 0;
                 }
-                added += gb_push_targets(j, ok, mbits, mcomp, tbits, hprow, mfn);
+                added += gb_push_targets(j, ok, mbits, mcomp, tbits, hprow, mfn, qbits);
             }
         }
     }
@@ -334,6 +374,7 @@ __device__ __forceinline__ long long gb_push_phase(int64_t nwords_u, const uint6
         const int64_t wl = w0 + (lane & 3);
         const uint64_t mine = wl < nwords_u ? ubits[wl] : 0;
         if (!__ballot(mine != 0)) continue;
+        if (qbits) adelta += gb_asg_words(g, w0, nwords_u, mine, lane);
         int64_t p0[4], d[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -373,7 +414,7 @@ __device__ __forceinline__ long long gb_push_phase(int64_t nwords_u, const uint6
                     j[u] = pcol[L.p[s] + (e - gb_wlist_start(L, s))];
                 }
             }
-            added += gb_push_targets(j, ok, mbits, mcomp, tbits, hprow, mfn);
+            added += gb_push_targets(j, ok, mbits, mcomp, tbits, hprow, mfn, qbits);
         }
         gb_wave_sync();
     }
@@ -393,7 +434,9 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
                                                       const uint64_t *__restrict__ mbits, bool mcomp,
                                                       uint64_t *__restrict__ tbits, gb_wlist &L,
                                                       const int64_t *__restrict__ hprow, long long &mfn,
-                                                      int p1_steps, int cap0, const uint64_t *__restrict__ rne) {
+                                                      int p1_steps, int cap0, const uint64_t *__restrict__ rne,
+                                                      const uint64_t *__restrict__ qbits, const gb_asg_dev &g,
+                                                      long long &adelta) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -404,7 +447,13 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
     for (int64_t w0 = wave * PULL_U; w0 < nwords; w0 += nwaves * PULL_U) {
         const int64_t wl = w0 + (lane & (PULL_U - 1));
         uint64_t mine = ~0ULL;
-        if (mbits) mine = wl < nwords ? (mcomp ? ~mbits[wl] : mbits[wl]) : 0;
+        if (qbits) {  // fused assign: w |= q; the mask is w's structure after it
+            const uint64_t qw = wl < nwords ? qbits[wl] : 0;
+            adelta += gb_asg_words(g, w0, nwords, qw, lane);
+            if (mbits) mine = wl < nwords ? (mcomp ? ~(mbits[wl] | qw) : (mbits[wl] | qw)) : 0;
+        } else if (mbits) {
+            mine = wl < nwords ? (mcomp ? ~mbits[wl] : mbits[wl]) : 0;
+        }
         if (rne && wl < nwords) mine &= rne[wl];  // rows without entries produce nothing
         if (wl == nwords - 1) mine &= tail;
         if (wl >= nwords) mine = 0;
@@ -615,6 +664,11 @@ struct gb_iso_args {
     // pull shape: lane-per-row steps of 4 edges, then the first per-row cap of the list rounds
     int p1_steps, cap0;
     const uint64_t *rows_nonempty;  // pull rows with entries (nullptr: all)
+    // fused deferred assign (gb_asg): w<q>(:) = x with q = u (asg.bits nullptr: none)
+    gb_asg_dev asg;
+    const void *asg_qiso;
+    int asg_qiso_code;
+    unsigned long long *asg_count;
 };
 
 // ------------------------------------------------ general SpMV: balanced words
@@ -1004,13 +1058,16 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
              w += (int64_t)gridDim.x * blockDim.x)
             a.spare[w] = 0;
     }
-    long long mfn = 0, cnt;
+    // fused assign: q's value mask is empty when q is iso with a false value
+    const uint64_t *qbits = nullptr;
+    if (a.asg.bits && (!a.asg_qiso || gb_dyn_nonzero(a.asg_qiso, a.asg_qiso_code))) qbits = ubits;
+    long long mfn = 0, cnt, adelta = 0;
     if (push)
         cnt = gb_push_phase(nwords_u, ubits, prow, pcol, hubs, nhubs, H, mbits, mcomp,
-                            (unsigned long long *)tbits, L, a.hprow, mfn);
+                            (unsigned long long *)tbits, L, a.hprow, mfn, qbits, a.asg, adelta);
     else
         cnt = gb_pull_iso_phase(nrows, rowptr, colidx, ubits, mbits, mcomp, tbits, L, a.hprow, mfn, a.p1_steps,
-                                a.cap0, a.rows_nonempty);
+                                a.cap0, a.rows_nonempty, qbits, a.asg, adelta);
     long long tot;
     if (gb_grid_sum(cnt, gst, &tot)) {
         *tcount = (unsigned long long)tot;
@@ -1025,6 +1082,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
         long long m;
         if (gb_grid_sum(mfn, gst + GB_GRID2_OFFSET, &m)) *a.mf_out = m;
     }
+    if (a.asg.bits) gb_grid_add(adelta, a.asg_count, gst + GB_GRID3_OFFSET);
 }
 
 // hub-chunk table of a CSR: pieces per row, then (row, piece) pairs
@@ -1146,7 +1204,7 @@ bool gb_spmv_result_iso(GrB_Semiring sr, bool a_iso, bool u_iso, bool flip) {
 }
 
 void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, gb_bitmap_view &u,
-             const gb_vmask &mask, GrB_Semiring sr, bool flip) {
+             const gb_vmask &mask, GrB_Semiring sr, bool flip, const gb_asg *asg) {
     gb_sr_info info = gb_sr_describe(sr);
     gb_scratch s;
     gb_csr_view &Av = const_cast<gb_csr_view &>(A);
@@ -1184,7 +1242,14 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             int64_t units = (nw + PULL_U - 1) / PULL_U;  // waves the pull wants
             std::lock_guard<std::mutex> lk(g_dir_mu);  // the spare bitmap and the direction state
             gb_iso_args args{};
-            args.rule = gb_dir_rule{mask.count, mask.comp, n, A.nvals, alpha, dir_knob == 2};
+            args.rule = gb_dir_rule{mask.count, asg ? u.count : nullptr, mask.comp, n, A.nvals, alpha, dir_knob == 2};
+            if (asg) {
+                GB_REQUIRE(u.n == n, GrB_INVALID_VALUE, "fused assign needs u and w of one size");
+                args.asg = gb_asg_dev{asg->bits, asg->vals, asg->size, asg->x};
+                args.asg_qiso = asg->q_iso;
+                args.asg_qiso_code = asg->q_iso_code;
+                args.asg_count = (unsigned long long *)asg->count;
+            }
             args.p1_steps = (int)gb_knob("pull_steps");
             if (args.p1_steps <= 0) args.p1_steps = 2;
             args.cap0 = (int)gb_knob("pull_cap");

@@ -6,6 +6,8 @@
 // Each call: validate -> views of the inputs (casting values to the operator's
 // input type) -> compute T on the device -> C<M,replace> = C accum T.
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 #include <vector>
 
 #include "gb_dispatch.cuh"
@@ -34,6 +36,9 @@ static void check_binop(GrB_BinaryOp op, bool allow_null) {
 }
 static int64_t ncols_of(GB_Obj *A) { return A->kind == GB_KIND_MATRIX ? A->ncols : 1; }
 
+static bool take_pending_assign(gb_asg &asg, GB_Obj *w, GB_Obj *mask, GB_Obj *A, GB_Obj *u, const gb_desc &d,
+                                bool iso_result);
+
 // ================================================================== mxv / vxm
 static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr, GB_Obj *A, GB_Obj *u,
                     const gb_desc &d, bool vxm) {
@@ -47,6 +52,14 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
     int64_t a_cols = (vxm ? (d.tran1 ? ncols_of(A) : A->nrows) : (d.tran0 ? A->nrows : ncols_of(A)));
     GB_REQUIRE(u->nrows == a_cols && ncols_of(u) == 1, GrB_DIMENSION_MISMATCH, "u size does not match A");
     GB_REQUIRE(w->nrows == a_rows && ncols_of(w) == 1, GrB_DIMENSION_MISMATCH, "w size does not match A");
+    // a deferred `mask<u> = x` (the BFS level stamp) is fused into this call's kernel, or done now
+    gb_asg asg;
+    bool fused = false;
+    if (g_pending_active.load(std::memory_order_acquire)) {
+        fused = A->kind == GB_KIND_MATRIX && u->kind != GB_KIND_MATRIX &&
+                take_pending_assign(asg, w, mask, A, u, d, gb_spmv_result_iso(sr, A->iso, u->iso, vxm));
+        if (!fused) gb_pending_flush();
+    }
     gb_csr_view av, pv;
     if (use_csc) gb_get_csc(av, A);
     else gb_get_csr(av, A);
@@ -76,7 +89,7 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
         T.pub = w->pub;
         T.pub_seq = gb_next_pub_seq();
     }
-    gb_spmv(T, av, push, uv, m, sr, vxm);
+    gb_spmv(T, av, push, uv, m, sr, vxm, fused ? &asg : nullptr);
     const void *hint_key = T.hint_key;
     const bool direct = gb_writeback_vector(w, T, mask, d, accum, true);
     if (direct && T.published) {
@@ -504,6 +517,25 @@ __global__ __launch_bounds__(OPS_BLOCK) void k_assign_mask_words(int64_t nwords,
     gb_grid_add(delta, count, gst);
 }
 
+// make a vector's value array writable in place (non-iso, allocated) and its count present
+static void make_values_writable(GB_Obj *w) {
+    const int64_t n = w->nrows;
+    const size_t ts = w->type->size;
+    if (!w->dense) {
+        w->dense = gb_malloc(n * ts);
+        w->iso = false;
+    } else if (w->iso) {
+        void *full = gb_expand_iso(w->dense, ts, n);
+        gb_free(w->dense);
+        w->dense = full;
+        w->iso = false;
+    }
+    if (!w->d_nvals) {
+        w->d_nvals = gb_malloc_n<int64_t>(1);
+        gb_memset(w->d_nvals, 0, sizeof(int64_t));
+    }
+}
+
 static bool assign_all_scalar_fast(GB_Obj *w, GB_Obj *mask, const char *xc, const gb_desc &d) {
     if (w->kind == GB_KIND_MATRIX) return false;
     const int64_t n = w->nrows;
@@ -527,20 +559,7 @@ static bool assign_all_scalar_fast(GB_Obj *w, GB_Obj *mask, const char *xc, cons
         gb_install_bitmap(w, n, bits, dense, true, cnt);
         return true;
     }
-    // make the value array writable (non-iso, allocated)
-    if (!w->dense) {
-        w->dense = gb_malloc(n * ts);
-        w->iso = false;
-    } else if (w->iso) {
-        void *full = gb_expand_iso(w->dense, ts, n);
-        gb_free(w->dense);
-        w->dense = full;
-        w->iso = false;
-    }
-    if (!w->d_nvals) {
-        w->d_nvals = gb_malloc_n<int64_t>(1);
-        gb_memset(w->d_nvals, 0, sizeof(int64_t));
-    }
+    make_values_writable(w);
     unsigned grid = (unsigned)std::min<int64_t>((n + OPS_BLOCK - 1) / OPS_BLOCK, 1024);
     gb_with_type(w->type->code, [&](auto z) {
         using T = decltype(z);
@@ -562,6 +581,65 @@ static bool assign_all_scalar_fast(GB_Obj *w, GB_Obj *mask, const char *xc, cons
     return true;
 }
 
+// ---- deferred masked scalar assign (gb_asg): `w<q>(:) = x` is recorded instead of
+// launched; the next GrB_mxv / GrB_vxm whose input is q and whose mask is w's
+// structure performs it inside its kernel (the BFS level loop, notebooks/Example
+// B.1 cell 8: v[:](mask=q.V) << d; q(~v.S, replace) << q.vxm(A)); any other API
+// call performs it first (gb_api -> gb_pending_flush), so the deferral is never
+// observable.  Knob fuse_assign = 1 disables it.
+std::atomic<bool> g_pending_active{false};
+static std::mutex g_pend_mu;
+static struct {
+    GB_Obj *w = nullptr, *mask = nullptr;
+    char x[16];
+    gb_desc d;
+} g_pend;
+
+void gb_pending_flush() {
+    std::lock_guard<std::mutex> lk(g_pend_mu);
+    GB_Obj *w = g_pend.w, *m = g_pend.mask;
+    g_pend.w = g_pend.mask = nullptr;
+    g_pending_active.store(false, std::memory_order_release);
+    if (w && w->magic == GB_MAGIC && m && m->magic == GB_MAGIC) assign_all_scalar_fast(w, m, g_pend.x, g_pend.d);
+}
+
+static bool try_defer_assign(GB_Obj *w, GB_Obj *mask, const char *xc, const gb_desc &d) {
+    if (gb_knob("fuse_assign") == 1) return false;
+    if (!mask || mask == w || w->kind == GB_KIND_MATRIX || mask->kind == GB_KIND_MATRIX) return false;
+    if (d.comp || d.replace || w->type->size > 8 || mask->nrows != w->nrows || !w->bits) return false;
+    if (!d.structure && !(mask->iso && mask->dense)) return false;  // per-entry values: assign now
+    make_values_writable(w);
+    std::lock_guard<std::mutex> lk(g_pend_mu);
+    g_pend.w = w;
+    g_pend.mask = mask;
+    memcpy(g_pend.x, xc, sizeof(g_pend.x));
+    g_pend.d = d;
+    g_pending_active.store(true, std::memory_order_release);
+    w->nvals_valid = false;
+    w->hint_valid = false;
+    return true;
+}
+
+// take the pending assign into `asg` when this SpMV can carry it out (see above)
+static bool take_pending_assign(gb_asg &asg, GB_Obj *w, GB_Obj *mask, GB_Obj *A, GB_Obj *u, const gb_desc &d,
+                                bool iso_result) {
+    std::lock_guard<std::mutex> lk(g_pend_mu);
+    GB_Obj *pw = g_pend.w;
+    if (!pw || pw != mask || g_pend.mask != u || !d.structure || w == pw || A == pw || !iso_result ||
+        u->kind == GB_KIND_MATRIX || pw->nrows != u->nrows)
+        return false;
+    asg.bits = pw->bits;
+    asg.vals = pw->dense;
+    asg.size = (int)pw->type->size;
+    memcpy(&asg.x, g_pend.x, sizeof(asg.x));
+    asg.q_iso = g_pend.d.structure ? nullptr : u->dense;
+    asg.q_iso_code = u->type->code;
+    asg.count = pw->d_nvals;
+    g_pend.w = g_pend.mask = nullptr;
+    g_pending_active.store(false, std::memory_order_release);
+    return true;
+}
+
 static void vector_assign_scalar(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, const void *x, int xcode,
                                  const GrB_Index *I, int64_t ni, const gb_desc &d) {
     check_binop(accum, true);
@@ -579,6 +657,7 @@ static void vector_assign_scalar(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, co
             memcpy(xc, &dv, sizeof(D));
         });
     });
+    if (I == GrB_ALL && !accum && try_defer_assign(w, mask, xc, d)) return;
     if (I == GrB_ALL && !accum && assign_all_scalar_fast(w, mask, xc, d)) return;
     gb_vec_result T;
     scalar_vec_T(T, w->nrows, I, ni, xc, ct);
@@ -820,7 +899,7 @@ GrB_Info GrB_mxm(GrB_Matrix C, const GrB_Matrix Mask, const GrB_BinaryOp accum, 
 
 GrB_Info GrB_mxv(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum, const GrB_Semiring op,
                  const GrB_Matrix A, const GrB_Vector u, const GrB_Descriptor desc) {
-    return gb_api(OBJ(w), [&] {
+    return gb_api_keep_pending(OBJ(w), [&] {
         do_spmv(gb_obj_check(w), gb_obj_check(mask, true), accum, op, gb_obj_check(A), gb_obj_check(u),
                 gb_read_desc(desc), false);
     });
@@ -828,7 +907,7 @@ GrB_Info GrB_mxv(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum, 
 
 GrB_Info GrB_vxm(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum, const GrB_Semiring op,
                  const GrB_Vector u, const GrB_Matrix A, const GrB_Descriptor desc) {
-    return gb_api(OBJ(w), [&] {
+    return gb_api_keep_pending(OBJ(w), [&] {
         do_spmv(gb_obj_check(w), gb_obj_check(mask, true), accum, op, gb_obj_check(A), gb_obj_check(u),
                 gb_read_desc(desc), true);
     });

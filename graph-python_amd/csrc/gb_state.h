@@ -7,4 +7,5 @@
 #define GB_GRID_STATE_WORDS ((GB_GRID_SHARDS + 1) * GB_GRID_STRIDE)
 #define GB_DIR_STATE_OFFSET GB_GRID_STATE_WORDS  // SpMV direction state (gb_mxv.hip)
 #define GB_GRID2_OFFSET (GB_GRID_STATE_WORDS + 32)  // a second grid-sum area (two sums in one kernel)
-#define GB_STATE_WORDS (GB_GRID2_OFFSET + GB_GRID_STATE_WORDS)
+#define GB_GRID3_OFFSET (GB_GRID2_OFFSET + GB_GRID_STATE_WORDS)  // a third one
+#define GB_STATE_WORDS (GB_GRID3_OFFSET + GB_GRID_STATE_WORDS)

@@ -645,3 +645,78 @@ def test_edge_cases(gb):
     M[3, 1] = 9
     del M[0, 0]
     assert M.to_dict() == {(3, 1): 9, (6, 1): 2}
+
+
+@pytest.mark.parametrize("fuse", [0, 1])
+@pytest.mark.parametrize("direction", [0, 1, 2])
+def test_bfs_fused_level_stamp(gb, fuse, direction):
+    """The level stamp v<q> = d is deferred and carried out inside the next vxm's kernel
+    (knob fuse_assign 0); with fuse_assign 1 it runs as its own launch.  Both must give
+    the oracle's levels."""
+    G = O.rmat(12, 16, 7)
+    r, c, _ = G.to_coo()
+    A = gb.Matrix.from_coo(r, c, True, nrows=G.nrows, ncols=G.ncols)
+    gb.set_knob("fuse_assign", fuse)
+    gb.set_knob("spmv_direction", direction)
+    try:
+        _bfs_check(gb, G, A)
+    finally:
+        gb.set_knob("fuse_assign", 0)
+        gb.set_knob("spmv_direction", 0)
+
+
+def _deferred_sequences(gb, seed):
+    """Sequences around a deferrable assign v<q>(:) = x whose results must not depend on
+    whether the assign is deferred / fused; returns the observable state."""
+    rng = np.random.default_rng(seed)
+    n = 700
+    G = O.rmat(9, 8, seed)
+    r, c, _ = G.to_coo()
+    P = gb.Matrix.from_coo(r, c, True, nrows=G.nrows, ncols=G.ncols)
+    n = G.nrows
+    out = []
+    for variant in ["fused", "read_v_between", "other_u", "struct_mask", "false_iso", "value_mask_noniso",
+                    "v_as_output", "twice"]:
+        v = gb.Vector(gb.INT32, n)
+        pre = rng.choice(n, 20, replace=False)
+        v.build(pre, np.arange(20, dtype=np.int32) + 100)
+        qi = rng.choice(n, 15, replace=False)
+        q = gb.Vector.from_coo(qi, False if variant == "false_iso" else True, dtype=bool, size=n)
+        if variant == "value_mask_noniso":
+            q = gb.Vector.from_coo(qi, (np.arange(15) % 2).astype(bool), dtype=bool, size=n)
+        mask = q.S if variant == "struct_mask" else q.V
+        v(mask=mask)[:] = 5
+        if variant == "read_v_between":
+            out.append(v.nvals)
+        if variant == "other_u":
+            u2 = gb.Vector.from_coo(rng.choice(n, 10, replace=False), True, dtype=bool, size=n)
+            q2 = u2.vxm(P, gb.semiring.lor_land).new(mask=~v.S)
+            out.append(q2.to_coo()[0])
+        elif variant == "v_as_output":
+            v(~v.S) << q.vxm(P, gb.semiring.plus_pair[gb.INT32])
+        elif variant == "twice":
+            v(mask=mask)[:] = 6
+            q(~v.S, replace=True) << q.vxm(P, gb.semiring.lor_land)
+        else:
+            q(~v.S, replace=True) << q.vxm(P, gb.semiring.lor_land)
+        out.append(q.to_coo()[0])
+        out.append(v.to_coo())
+        out.append(v.nvals)
+    return out
+
+
+def test_deferred_assign_is_unobservable(gb):
+    results = []
+    for fuse in (1, 0):
+        gb.set_knob("fuse_assign", fuse)
+        try:
+            results.append(_deferred_sequences(gb, 3))
+        finally:
+            gb.set_knob("fuse_assign", 0)
+    a, b = results
+    assert len(a) == len(b)
+    for x, y in zip(a, b):
+        if isinstance(x, tuple):
+            assert np.array_equal(x[0], y[0]) and np.array_equal(x[1], y[1])
+        else:
+            assert np.array_equal(np.asarray(x), np.asarray(y))
