@@ -59,6 +59,10 @@ def parse():
     p.add_argument("--dist-backend", default="nccl")
     p.add_argument("--device", type=int, default=None, help="override LOCAL_RANK's device")
     p.add_argument("--knob", action="append", default=[], help="library knob key=value (ablations)")
+    p.add_argument("--spgemm-scale", type=int, default=19, help="config 5 (unmasked fp64 SpGEMM) R-MAT scale")
+    p.add_argument("--spgemm-steps", type=int, default=2)
+    p.add_argument("--spgemm-warmup", type=int, default=1)
+    p.add_argument("--no-spgemm", action="store_true", help="skip the config 5 line")
     return p.parse_args()
 
 
@@ -217,6 +221,126 @@ def secondary_workloads(lib, torch, stream, O, args):
     for h in (B, C):
         lib.GrB_Matrix_free(ctypes.byref(h))
     return out
+
+
+def config5_spgemm(lib, torch, stream, dist, world, rank, args):
+    """SURVEY 8(d) config 5 / 8(e) mxm row: C = A plus.times A, FP64, unmasked, on R-MAT
+    (scale args.spgemm_scale; s23 does not fit 8 x 288 GB), 1-D row shards.
+    Rank r holds rows [lo, hi) of A (generated as a row shard), which is also its panel of B;
+    one step = the all-gatherv of B's CSR row panels over RCCL (dist.RowPanelAllGather, on the
+    library stream) + GxB_Matrix_import_device + the local GrB_mxm(C_r, A_r, B).  Total work is
+    fixed as N grows.  GTEPS = products (sum over A's entries (i,k) of |B(k,:)|) / max-over-ranks
+    time.  Parity: 16 sampled rows of each rank's C_r against a numpy fold of the same rows
+    (fp64, rtol 1e-6; structure exact)."""
+    from graphblas_amd import device as gdev
+    from graphblas_amd import dist as gdist
+
+    sc = args.spgemm_scale
+    n = 1 << sc
+    part = gdist.partition(n, world, rank)
+    lo, hi = part["lo"], part["hi"]
+    A = ctypes.c_void_p()
+    ok(lib.GxB_Matrix_rmat(ctypes.byref(A), sc, args.edge_factor, args.seed, 2, 2, lo, hi), "rmat fp64 row panel")
+    torch.cuda.synchronize()
+    va = gdev.matrix_view(A)
+    nr, nnz_a = va.nrows, va.nvals
+    gath = gdist.RowPanelAllGather(dist, world, rank) if world > 1 else None
+    sr = lib.GrB_PLUS_TIMES_SEMIRING_FP64
+    nv = ctypes.c_uint64()
+    keep = {}
+
+    def step(keep_c=False):
+        if world > 1:
+            with torch.cuda.stream(stream):
+                B, brp = gdist.gather_row_panels(lib, torch, gath, A, n)
+        else:
+            B = A
+        C = ctypes.c_void_p()
+        ok(lib.GrB_Matrix_new(ctypes.byref(C), lib.GrB_FP64, nr, n), "C")
+        ok(lib.GrB_mxm(C, None, None, sr, A, B, None), "mxm")
+        ok(lib.GrB_Matrix_nvals(ctypes.byref(nv), C), "nvals C")
+        if keep_c:
+            keep["C"], keep["B"] = C, B
+        else:
+            ok(lib.GrB_Matrix_free(ctypes.byref(C)), "free C")
+            if world > 1:
+                ok(lib.GrB_Matrix_free(ctypes.byref(B)), "free B")
+        return nv.value
+
+    # untimed: one step kept for the product count and the parity sample
+    nnz_c = step(keep_c=True)
+    B = keep["B"]
+    vb = gdev.matrix_view(B)
+    brp = gdev.device_tensor(torch, vb.rowptr, n + 1)
+    deg = brp[1:] - brp[:-1]
+    aci = gdev.device_tensor(torch, va.colidx, nnz_a, "<i4").long()
+    prods = int(deg[aci].sum().item())
+    # parity sample (host): rows of C_r vs a numpy fold over A_r and B
+    C = keep["C"]
+    vc = gdev.matrix_view(C)
+    crp = gdev.device_tensor(torch, vc.rowptr, nr + 1).cpu().numpy()
+    arp = gdev.device_tensor(torch, va.rowptr, nr + 1).cpu().numpy()
+    ax = gdev.device_tensor(torch, va.values, nnz_a, "<f8").cpu().numpy()
+    ai = aci.cpu().numpy()
+    bp = brp.cpu().numpy()
+    bi = gdev.device_tensor(torch, vb.colidx, vb.nvals, "<i4").cpu().numpy()
+    bx = gdev.device_tensor(torch, vb.values, vb.nvals, "<f8").cpu().numpy()
+    cit = gdev.device_tensor(torch, vc.colidx, vc.nvals, "<i4")
+    cvt = gdev.device_tensor(torch, vc.values, vc.nvals, "<f8")
+    rows = np.sort(np.random.default_rng(11 + rank).choice(nr, min(16, nr), replace=False)) if nr else []
+    parity = True
+    for r in rows:
+        acc = np.zeros(n)
+        present = np.zeros(n, bool)
+        for p in range(arp[r], arp[r + 1]):
+            k = ai[p]
+            s, e = bp[k], bp[k + 1]
+            acc[bi[s:e]] += ax[p] * bx[s:e]
+            present[bi[s:e]] = True
+        cols = np.flatnonzero(present)
+        gc = cit[crp[r]:crp[r + 1]].cpu().numpy()
+        gv = cvt[crp[r]:crp[r + 1]].cpu().numpy()
+        parity &= bool(np.array_equal(gc, cols) and np.allclose(gv, acc[cols], rtol=1e-6, atol=0))
+    ok(lib.GrB_Matrix_free(ctypes.byref(C)), "free C")
+    if world > 1:
+        ok(lib.GrB_Matrix_free(ctypes.byref(B)), "free B")
+    for _ in range(args.spgemm_warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.spgemm_steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / args.spgemm_steps
+    tot = [prods, nnz_c, nnz_a, int(parity)]
+    if dist:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        tt = torch.tensor(tot[:3] + [1 - tot[3]], dtype=torch.int64, device="cuda")
+        dist.all_reduce(tt)
+        tot = [int(x) for x in tt.tolist()]
+        tot[3] = int(tot[3] == 0)
+    prods_all, nnzc_all, nnza_all, par_all = tot
+    # bytes per step (SURVEY 8(d) config 5): A and B as CSR read, C written, the panels' exchange
+    by = 2 * (12 * nnza_all + 8 * (n + 1)) + 12 * nnzc_all + 8 * (n + 1)
+    if world > 1:
+        by += world * (12 * nnza_all + 8 * n)  # every rank receives the whole B
+    ok(lib.GrB_Matrix_free(ctypes.byref(A)), "free A")
+    return {
+        "workload": f"C = A plus.times A (GrB_mxm, unmasked, FP64 U[0,1)), R-MAT s{sc} ef {args.edge_factor}, "
+                    f"1-D row shards x{world}, B row panels all-gathered over "
+                    f"{'RCCL' if world > 1 else '(none: one GPU)'}",
+        "n": n, "nnz_A": nnza_all, "nnz_C": nnzc_all, "products": prods_all, "ms": el * 1e3,
+        "gteps": prods_all / el / 1e9, "gteps_def": "products (sum over A(i,k) of |B(k,:)|) per second",
+        "alg_bytes": by, "hbm_GBs_per_gpu": by / world / el / 1e9, "parity_sampled_rows": bool(par_all),
+        "steps": args.spgemm_steps, "warmup": args.spgemm_warmup, "scaling": "strong"}
 
 
 def main():
@@ -462,9 +586,11 @@ def main():
         copy_gbs = 5 * 2 * xs.numel() / (time.perf_counter() - c0) / 1e9
         del xs, ys
 
-    secondary = None
+    secondary = {}
     if rank == 0 and world == 1 and not args.no_secondary:
         secondary = secondary_workloads(lib, torch, stream, O, args)
+    if not args.no_spgemm:
+        secondary["config5_spgemm_plus_times_fp64"] = config5_spgemm(lib, torch, stream, dist, world, rank, args)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -385,6 +385,9 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
 bool gb_spmv_result_iso(GrB_Semiring sr, bool a_iso, bool u_iso, bool flip);
 void gb_spgemm(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, gb_csr_view *BT,
                gb_mmask &mask, GrB_Semiring sr);
+// hash Gustavson C = A*B (gb_spgemm_hash.hip): flops = per-row product counts
+void gb_spgemm_hash(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, GrB_Semiring sr, bool iso,
+                    const void *av, const void *bv, const int64_t *flops);
 
 // scans / sorts (gb_prim.hip)
 void gb_exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n);  // out[n] = total

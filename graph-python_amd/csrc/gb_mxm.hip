@@ -12,7 +12,8 @@
 //    without disturbing their k order, and one pass folds each run.  Rows are
 //    processed in chunks so the expanded products stay within a memory budget.
 // Both fold every output entry in ascending k, so floating-point results do
-// not depend on scheduling.
+// not depend on scheduling.  The default Gustavson kernel is the hash method of
+// gb_spgemm_hash.hip; expand-sort-compress is kept behind knob spgemm_method=1.
 #include <algorithm>
 #include <vector>
 
@@ -390,6 +391,21 @@ void gb_spgemm(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, gb_csr_view *BT
         hipLaunchKernelGGL(k_row_flops, dim3(mxm_grid(std::min<int64_t>(nrows * 64, 1LL << 22))), dim3(MXM_BLOCK), 0,
                            gb_stream(), A.rowptr, A.colidx, nrows, B.rowptr, fl);
     GB_LAUNCH_CHECK();
+    if (gb_knob("spgemm_method") != 1) {
+        // default: hash Gustavson (gb_spgemm_hash.hip)
+        gb_spgemm_hash(T, A, B, sr, iso, av, bv, fl);
+        if (iso)
+            gb_dispatch_sr(info, [&](auto srf, auto x, auto z) {
+                using SRT = decltype(srf);
+                using X = decltype(x);
+                using Z = decltype(z);
+                hipLaunchKernelGGL((k_iso_value2<SRT, X, Z>), dim3(1), dim3(1), 0, gb_stream(), srf, (const X *)av,
+                                   (const X *)bv, (Z *)T.vals);
+                GB_LAUNCH_CHECK();
+            });
+        T.within_mask = false;
+        return;
+    }
     gb_exclusive_scan_i64(fl, flp, nrows);
     const int64_t F = gb_read_i64(flp + nrows);
     int64_t budget = gb_knob("esc_budget");

@@ -1357,6 +1357,40 @@ GrB_Info GxB_Matrix_device_view(GxB_DeviceView *view, const GrB_Matrix A) {
         }
     });
 }
+// CSR from device buffers (copied on the library stream): the receiving side of
+// an all-gather of row panels (graphblas_amd.dist.gather_row_panels).  The caller
+// guarantees a valid CSR (rowptr[0] == 0, sorted unique columns per row), the
+// contract of GxB_Matrix_import_CSR with jumbled = false.
+GrB_Info GxB_Matrix_import_device(GrB_Matrix *A, GrB_Type type, GrB_Index nrows, GrB_Index ncols,
+                                  const void *rowptr, const void *colidx, const void *values,
+                                  GrB_Index nvals, bool iso) {
+    if (!A) return GrB_NULL_POINTER;
+    return gb_api(nullptr, [&] {
+        GB_REQUIRE(type && type->magic == GB_MAGIC, GrB_UNINITIALIZED_OBJECT, "type");
+        GB_REQUIRE(rowptr && (nvals == 0 || colidx) && (nvals == 0 || values), GrB_NULL_POINTER,
+                   "device buffers");
+        GB_REQUIRE(ncols <= (GrB_Index)INT32_MAX, GrB_INVALID_VALUE, "ncols exceeds the 32-bit column index");
+        GB_Obj *o = gb_new_object(GB_KIND_MATRIX, type, (int64_t)nrows, (int64_t)ncols);
+        try {
+            const size_t zs = gb_type_size(type->code);
+            int64_t *rp = gb_malloc_n<int64_t>(nrows + 1);
+            int32_t *ci = gb_malloc_n<int32_t>(nvals ? nvals : 1);
+            const bool is = iso && nvals > 0;
+            void *vx = gb_malloc((is ? 1 : (nvals ? nvals : 1)) * zs);
+            gb_copy_d2d(rp, rowptr, (nrows + 1) * sizeof(int64_t));
+            if (nvals) {
+                gb_copy_d2d(ci, colidx, nvals * sizeof(int32_t));
+                gb_copy_d2d(vx, values, (is ? 1 : nvals) * zs);
+            }
+            gb_install_csr(o, (int64_t)nrows, (int64_t)ncols, (int64_t)nvals, rp, ci, vx, is);
+        } catch (...) {
+            GrB_Matrix m = (GrB_Matrix)o;
+            GrB_Matrix_free(&m);
+            throw;
+        }
+        *A = (GrB_Matrix)o;
+    });
+}
 GrB_Info GxB_Vector_device_view(GxB_DeviceView *view, const GrB_Vector v) {
     return GxB_Matrix_device_view(view, (GrB_Matrix)v);
 }

@@ -59,6 +59,7 @@ _SIGS = {
     "GxB_Vector_device_touch": [P], "GxB_Matrix_prepare_transpose": [P],
     "GxB_Matrix_rmat": [P, E, E, U, E, U, I, I],
     "GxB_Vector_bitmap_export": [P, P, I], "GxB_Vector_bitmap_import": [P, P, I],
+    "GxB_Matrix_import_device": [P, P, I, I, P, P, P, I, ctypes.c_bool],
 }
 for _t in TYPE_NAMES:
     _T = _CTYPES[_t]

@@ -30,3 +30,11 @@ class _CudaArray:
 def device_tensor(torch, ptr, n, typestr="<i8"):
     """A torch tensor aliasing n elements of library device memory (no copy)."""
     return torch.as_tensor(_CudaArray(ptr, n, typestr), device="cuda")
+
+
+def matrix_view(handle):
+    v = DeviceView()
+    rc = lib.GxB_Matrix_device_view(ctypes.byref(v), handle)
+    if rc != 0:
+        raise RuntimeError(f"GxB_Matrix_device_view failed: {rc}")
+    return v

@@ -325,6 +325,14 @@ typedef struct {
 } GxB_DeviceView;
 GrB_Info GxB_Matrix_device_view(GxB_DeviceView *view, const GrB_Matrix A);
 GrB_Info GxB_Vector_device_view(GxB_DeviceView *view, const GrB_Vector v);
+/* Build a CSR matrix from device buffers (copied on the library stream):
+ * rowptr int64[nrows+1] (rowptr[0] = 0), colidx int32[nvals] sorted and unique per
+ * row, values typed [nvals] or [1] when iso.  Receives all-gathered row panels
+ * (1-D row-sharded GrB_mxm); the device-side counterpart of
+ * GxB_Matrix_import_CSR (reference core/ss/matrix.py:1282-1352). */
+GrB_Info GxB_Matrix_import_device(GrB_Matrix *A, GrB_Type type, GrB_Index nrows, GrB_Index ncols,
+                                  const void *rowptr, const void *colidx, const void *values,
+                                  GrB_Index nvals, bool iso);
 /* Mark that the vector's bitmap/values were rewritten through a device view
  * (nvals recomputed on device, on the library stream). */
 GrB_Info GxB_Vector_device_touch(GrB_Vector v);

@@ -1,0 +1,99 @@
+"""Row-sharded SpGEMM exchange at world_size 2 and 3 on CPU (gloo): each rank holds a
+consecutive block of rows of A (= its panel of B, since C = A*A); the CSR row panels
+are all-gathered (graphblas_amd.dist.RowPanelAllGather: sizes, then one broadcast per
+owner straight into the assembled buffers) and the local product C_r = A_r plus.times B
+(here the oracle; GrB_mxm on the GPU, bench.py config 5) stacked over the ranks must
+equal the oracle's A plus.times A.  SURVEY §8(e) mxm row; DESIGN.md §6."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle as O
+from graphblas_amd import dist as gdist
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, scale, ef, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    G = O.rmat(scale, ef, 42, values="FP64", value_seed=2)
+    n = G.nrows
+    part = gdist.partition(n, world, rank)
+    lo, hi = part["lo"], part["hi"]
+    p0, p1 = int(G.indptr[lo]), int(G.indptr[hi])
+    rp = torch.from_numpy(G.indptr[lo:hi + 1] - p0)
+    ci = torch.from_numpy(G.indices[p0:p1].astype(np.int32))
+    vx = torch.from_numpy(G.values[p0:p1].copy())
+    brp, bci, bvx = gdist.RowPanelAllGather(dist, world, rank).run(rp, ci, vx)
+    B = O.Csr(n, n, "FP64", brp.numpy(), bci.numpy(), bvx.numpy())
+    Ar = O.Csr(hi - lo, n, "FP64", rp.numpy(), ci.numpy(), vx.numpy())
+    C = O.mxm(O.Csr.empty(hi - lo, n, "FP64"), Ar, B, ("PLUS", "TIMES", "FP64"))
+    out_q.put((rank, lo, hi, brp.numpy(), bci.numpy(), bvx.numpy(), C.indptr, C.indices, C.values))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,scale,ef", [(2, 8, 8), (3, 9, 8), (2, 6, 4)])
+def test_row_panel_spgemm_matches_oracle(world, scale, ef):
+    G = O.rmat(scale, ef, 42, values="FP64", value_seed=2)
+    ref = O.mxm(O.Csr.empty(G.nrows, G.ncols, "FP64"), G, G, ("PLUS", "TIMES", "FP64"))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, scale, ef, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # every rank assembled exactly A (scale 6 with 2 ranks: rank 1 holds an empty panel)
+    for _, lo, hi, brp, bci, bvx, _, _, _ in res:
+        assert np.array_equal(brp, G.indptr) and np.array_equal(bci.astype(np.int64), G.indices)
+        assert np.array_equal(bvx, G.values)
+    # the stacked row panels of C are the oracle's C (the same fold order: bit-exact)
+    cp = [np.zeros(1, np.int64)]
+    ci, cv = [], []
+    base = 0
+    for _, lo, hi, _, _, _, rp, idx, val in res:
+        cp.append(rp[1:] + base)
+        base += int(rp[-1])
+        ci.append(idx)
+        cv.append(val)
+    assert np.array_equal(np.concatenate(cp), ref.indptr)
+    assert np.array_equal(np.concatenate(ci), ref.indices)
+    assert np.array_equal(np.concatenate(cv), ref.values)
+
+
+def test_row_panel_world1_and_iso():
+    """world 1 (no collective issued): the panel comes back as is; iso panels keep one value."""
+
+    class _One:
+        def all_gather(self, out, t):
+            out[0].copy_(t)
+
+        def broadcast(self, t, src):
+            raise AssertionError("no broadcast at world 1")
+
+    G = O.rmat(7, 8, 42, values="FP64", value_seed=2)
+    rp = torch.from_numpy(G.indptr.copy())
+    ci = torch.from_numpy(G.indices.astype(np.int32))
+    vx = torch.from_numpy(G.values.copy())
+    brp, bci, bvx = gdist.RowPanelAllGather(_One(), 1, 0).run(rp, ci, vx)
+    assert np.array_equal(brp.numpy(), G.indptr) and np.array_equal(bci.numpy(), ci.numpy())
+    assert np.array_equal(bvx.numpy(), G.values)
+    one = torch.ones(1, dtype=torch.float64)
+    _, _, ivx = gdist.RowPanelAllGather(_One(), 1, 0).run(rp, ci, one, iso=True)
+    assert ivx.numel() == 1 and float(ivx[0]) == 1.0

@@ -11,6 +11,7 @@ test_vxm_nonsquare :309, test_vxm_mask :323, test_vxm_accum :348,
 test_inner :1479, test_outer :1521; graphblas/tests/test_infix.py :80;
 graphblas/tests/test_recorder.py :15; docs/user_guide/operations.rst:24-148.
 """
+import contextlib
 import numpy as np
 import pytest
 
@@ -317,6 +318,17 @@ def _rand_csr(rng, n, m, density, dtype):
     return O.Csr.from_coo(r, c, vals, nrows=n, ncols=m, dtype=dtype)
 
 
+@contextlib.contextmanager
+def _knobs(gb, **kv):
+    for k, v in kv.items():
+        gb.set_knob(k, v)
+    try:
+        yield
+    finally:
+        for k in kv:
+            gb.set_knob(k, 0)
+
+
 def _to_gb(gb, M):
     r, c, v = M.to_coo()
     return gb.Matrix.from_coo(r, c, v, dtype=M.dtype, nrows=M.nrows, ncols=M.ncols)
@@ -586,16 +598,48 @@ def test_masked_spgemm_rmat_vs_oracle(gb, scale):
     _check_mat(C, ref)
 
 
+@pytest.mark.parametrize("method", ["hash", "hash_window", "esc"])
 @pytest.mark.parametrize("scale", [9, 11])
-def test_unmasked_spgemm_fp64_rmat_vs_oracle(gb, scale):
+def test_unmasked_spgemm_fp64_rmat_vs_oracle(gb, scale, method):
     G = O.rmat(scale, 8, 42, values="FP64", value_seed=2)
     A = _to_gb(gb, G)
-    C = A.mxm(A, gb.semiring.plus_times).new()
+    with _knobs(gb, spgemm_method=1 if method == "esc" else 0, hash_window=int(method == "hash_window")):
+        C = A.mxm(A, gb.semiring.plus_times).new()
     ref = O.mxm(O.Csr.empty(G.nrows, G.ncols, "FP64"), G, G, ("PLUS", "TIMES", "FP64"))
     _check_mat(C, ref, fp=True)
-    # the expand-sort-compress path folds in ascending k: bit-identical to the oracle
-    r, c, vv = C.to_coo()
-    assert np.array_equal(vv, ref.values)
+    if method == "esc":
+        # the expand-sort-compress path folds in ascending k: bit-identical to the oracle
+        r, c, vv = C.to_coo()
+        assert np.array_equal(vv, ref.values)
+
+
+UNMASKED_SR = [s for s in SEMIRINGS if s[1] != "ANY"] + [("any_pair", "ANY", "PAIR", "BOOL")]
+
+
+@pytest.mark.parametrize("name,mon,mul,dt", UNMASKED_SR)
+@pytest.mark.parametrize("method", ["hash", "hash_window"])
+def test_hash_spgemm_rmat_vs_oracle(gb, name, mon, mul, dt, method):
+    """Hash Gustavson on R-MAT s12 (rows in every bin: wave / workgroup LDS tables and, for
+    the hub rows or with hash_window, the column-window kernel) against the oracle: bit-exact for exact
+    monoids, rtol 1e-6 for floating plus / times (summation order)."""
+    G = O.rmat(12, 16, 7, values="INT64" if dt != "BOOL" else None, value_seed=5)
+    if dt != "BOOL":
+        vals = (G.values % 13 + 1).astype(O.NP[dt]) if dt not in ("FP32", "FP64") else \
+            (G.values.astype(np.float64) / 7.0).astype(O.NP[dt])
+    else:
+        vals = np.ones(G.nvals, bool)
+    G = O.Csr(G.nrows, G.ncols, dt, G.indptr, G.indices, vals)
+    A = _to_gb(gb, G)
+    sr = getattr(gb.semiring, name)[dt]
+    with _knobs(gb, hash_window=int(method == "hash_window")):
+        C = A.mxm(A, sr).new()
+    ref = O.mxm(O.Csr.empty(G.nrows, G.ncols, dt), G, G, (mon, mul, dt))
+    if mon == "ANY":
+        r, c, _ = C.to_coo()
+        er, ec, _ = ref.to_coo()
+        assert np.array_equal(r.astype(np.int64), er) and np.array_equal(c.astype(np.int64), ec)
+    else:
+        _check_mat(C, ref, fp=dt in ("FP32", "FP64") and mon in ("PLUS", "TIMES"))
 
 
 def test_spmv_fp64_rmat_vs_scipy(gb):
