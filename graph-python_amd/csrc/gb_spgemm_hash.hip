@@ -408,7 +408,8 @@ __device__ __forceinline__ int64_t gallop_lb(const int32_t *__restrict__ ci, int
 
 template <bool SYM, bool VALS, class SR, class X, class Z>
 __global__ __launch_bounds__(HG) void k_row_window(
-    SR sr, int mon, const int32_t *__restrict__ rows, int64_t nr, int logW, int vcap, int64_t *__restrict__ cur,
+    SR sr, int mon, const int32_t *__restrict__ rows, int64_t nr, int logW, int vcap, int in_c_groups,
+    int64_t *__restrict__ cur,
     const int64_t *__restrict__ arp, const int32_t *__restrict__ aci, const X *__restrict__ avx, bool a_iso,
     const int64_t *__restrict__ brp, const int32_t *__restrict__ bci, const X *__restrict__ bvx, bool b_iso,
     int64_t ncols, int64_t *__restrict__ cnt, const int64_t *__restrict__ crp, int32_t *__restrict__ cci,
@@ -588,7 +589,33 @@ __global__ __launch_bounds__(HG) void k_row_window(
                         }
                         return lo;
                     };
-                    const int ng = (int)(chunk_pre(NB - 1) / G) + 1;
+                    // more than in_c_groups groups of LDS value slots and a slot as wide as a
+                    // value: one sweep accumulating straight into C's values (this row's output
+                    // range, L2-resident) instead of one sweep per group; 1-2-byte values use
+                    // 4-byte slots and keep the grouped path
+                    constexpr bool IN_C = sizeof(S) == sizeof(Z);
+                    const int ngg = (int)(chunk_pre(NB - 1) / G) + 1;
+                    const bool in_c = IN_C && ngg > in_c_groups;
+                    const int ng = in_c ? 0 : ngg;
+                    if (in_c) {
+                        S *dst = (S *)(cvx + outpos);
+                        if (has_id)
+                            for (int64_t q = tid; q < m; q += HG) dst[q] = ids;
+                        __syncthreads();
+                        mn = sweep(
+                            [&](int64_t pb, int32_t k, X av) {
+                                const int32_t j = bci[pb];
+                                X bv = X();
+                                if (rv) bv = bvx[b_iso ? 0 : pb];
+                                const Z z = sr.mult(av, bv, i, k, j);
+                                const int32_t c = j - c0;
+                                const int32_t rk = prew[c >> 5] + __popc(bm[c >> 5] & ((1u << (c & 31)) - 1u));
+                                if (mon == GBAMD_MON_ANY) dst[rk] = to_slot<Z, S>(z);
+                                else slot_accum<SR, Z, S>(sr, mon, dst + rk, z);
+                            },
+                            c1, true);
+                        __syncthreads();
+                    }
                     for (int g = 0; g < ng; g++) {
                         const int bs = first_chunk((int64_t)g * G), be = first_chunk((int64_t)(g + 1) * G);
                         const int64_t rbase = chunk_pre(bs), rcnt = chunk_pre(be) - rbase;
@@ -782,11 +809,17 @@ void gb_spgemm_hash(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, GrB_Semiri
                 // prefixes 32 KB) with values in LDS in groups of < 8192 entries (64 KB for 8-byte
                 // values; one-to-two-byte values: a group can hold the whole window)
                 const int lw = SYM ? win_log(19) : (sizeof(Z) < 4 ? win_log(13) : win_log(17));
-                const int vcap = (SYM || !VALS) ? 0 : (sizeof(Z) < 4 ? (1 << lw) : 8192);
+                int vcap = (SYM || !VALS) ? 0 : (sizeof(Z) < 4 ? (1 << lw) : 8192);
+                // tests: a small LDS value capacity sends windows to the C-resident accumulation
+                const int64_t kv = gb_knob("window_vcap");
+                if (vcap && kv > 256 && kv < vcap) vcap = (int)kv;
+                // grouped sweeps (one per vcap entries) up to this many, then C-resident accumulation
+                const int64_t kg = gb_knob("window_in_c_groups");
+                const int in_c_groups = kg > 0 ? (int)kg : 8;  // tools/sweep_in_c.sh: 2 226 ms, 4 208, 8 204, never 206 (config 5)
                 const size_t sh = SYM ? (size_t)(1 << lw) / 8 : (size_t)(1 << lw) / 4 + (size_t)vcap * sizeof(S);
                 set_lds(k_row_window<SYM, VALS, SRT, X, Z>, sh);
                 hipLaunchKernelGGL((k_row_window<SYM, VALS, SRT, X, Z>), dim3(hgrid(b.c[4], 1, 2048)), dim3(HG), sh,
-                                   gb_stream(), srf, mon, rows + b.st[4], b.c[4], lw, vcap, cur, A.rowptr, A.colidx,
+                                   gb_stream(), srf, mon, rows + b.st[4], b.c[4], lw, vcap, in_c_groups, cur, A.rowptr, A.colidx,
                                    ax, A.iso, B.rowptr, B.colidx, bx, B.iso, ncols, cnt, crp, wci, wvx);
             }
             GB_LAUNCH_CHECK();

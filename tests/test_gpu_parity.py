@@ -617,10 +617,11 @@ UNMASKED_SR = [s for s in SEMIRINGS if s[1] != "ANY"] + [("any_pair", "ANY", "PA
 
 
 @pytest.mark.parametrize("name,mon,mul,dt", UNMASKED_SR)
-@pytest.mark.parametrize("method", ["hash", "hash_window"])
+@pytest.mark.parametrize("method", ["hash", "hash_window", "hash_window_c"])
 def test_hash_spgemm_rmat_vs_oracle(gb, name, mon, mul, dt, method):
     """Hash Gustavson on R-MAT s12 (rows in every bin: wave / workgroup LDS tables and, for
-    the hub rows or with hash_window, the column-window kernel) against the oracle: bit-exact for exact
+    the hub rows or with hash_window, the column-window kernel; hash_window_c shrinks the window's
+    LDS value capacity so windows accumulate in C's values) against the oracle: bit-exact for exact
     monoids, rtol 1e-6 for floating plus / times (summation order)."""
     G = O.rmat(12, 16, 7, values="INT64" if dt != "BOOL" else None, value_seed=5)
     if dt != "BOOL":
@@ -631,7 +632,8 @@ def test_hash_spgemm_rmat_vs_oracle(gb, name, mon, mul, dt, method):
     G = O.Csr(G.nrows, G.ncols, dt, G.indptr, G.indices, vals)
     A = _to_gb(gb, G)
     sr = getattr(gb.semiring, name)[dt]
-    with _knobs(gb, hash_window=int(method == "hash_window")):
+    with _knobs(gb, hash_window=int(method != "hash"), window_vcap=512 if method == "hash_window_c" else 0,
+                window_in_c_groups=1 if method == "hash_window_c" else 0):
         C = A.mxm(A, sr).new()
     ref = O.mxm(O.Csr.empty(G.nrows, G.ncols, dt), G, G, (mon, mul, dt))
     if mon == "ANY":
