@@ -111,6 +111,9 @@ struct GB_Matrix_opaque {
     bool hint_valid;
     const void *hint_key;
     std::string err;
+    // set when a deferred operation on this object failed after its call returned
+    // (GrB_INVALID_OBJECT from then on, C API 2.0 nonblocking execution errors)
+    GrB_Info invalid = GrB_SUCCESS;
 };
 typedef GB_Matrix_opaque GB_Obj;
 
@@ -391,6 +394,7 @@ void gb_spgemm_hash(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, GrB_Semiri
 
 // scans / sorts (gb_prim.hip)
 void gb_exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n);  // out[n] = total
+void gb_exclusive_scan_u8(const uint8_t *in, int64_t *out, int64_t n);  // 0/1 flags, int64 prefixes
 void gb_sort_pairs_u64(uint64_t *keys, int64_t *vals, int64_t n, int end_bit);
 void gb_sort_pairs_i32(int32_t *keys, int64_t *vals, int64_t n, int end_bit);
 int64_t gb_read_i64(const int64_t *dptr);

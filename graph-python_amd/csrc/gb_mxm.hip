@@ -11,9 +11,14 @@
 //    a stable radix sort on (i, j) groups the terms of each output entry
 //    without disturbing their k order, and one pass folds each run.  Rows are
 //    processed in chunks so the expanded products stay within a memory budget.
-// Both fold every output entry in ascending k, so floating-point results do
-// not depend on scheduling.  The default Gustavson kernel is the hash method of
-// gb_spgemm_hash.hip; expand-sort-compress is kept behind knob spgemm_method=1.
+// The masked dot kernels and expand-sort-compress fold every output entry in
+// ascending k, so their floating-point results do not depend on scheduling.
+// The default Gustavson kernel is the hash method of gb_spgemm_hash.hip, which
+// folds fp PLUS/TIMES with atomics in arrival order: fp64 plus_times results
+// can differ between runs in the last bits (exact monoids -- min/max/integer
+// plus/times/lor/land/any_pair -- stay bit-exact).  Knob spgemm_method=1
+// (GxB_set_knob, graphblas_amd.set_knob("spgemm_method", 1)) selects
+// expand-sort-compress: the deterministic, bit-reproducible mode.
 #include <algorithm>
 #include <vector>
 

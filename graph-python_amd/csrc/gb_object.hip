@@ -49,6 +49,7 @@ GB_Obj *gb_obj_check(const void *p, bool allow_null) {
     GB_Obj *A = OBJ(p);
     if (A->magic == GB_FREED) gb_throw(GrB_INVALID_OBJECT, "object has been freed");
     if (A->magic != GB_MAGIC) gb_throw(GrB_UNINITIALIZED_OBJECT, "object is not initialized");
+    if (A->invalid != GrB_SUCCESS) gb_throw(GrB_INVALID_OBJECT, A->err);
     return A;
 }
 

@@ -595,12 +595,29 @@ static struct {
     gb_desc d;
 } g_pend;
 
+// A failure of the deferred assign is an execution error of `w`, not of the call that
+// triggered the flush: it is recorded on w (message + GrB_INVALID_OBJECT from then on,
+// as the C API 2.0 prescribes for nonblocking execution errors) and the triggering call
+// goes on.  The pending record is cleared only once the assign has been issued or has
+// failed and been recorded.
 void gb_pending_flush() {
     std::lock_guard<std::mutex> lk(g_pend_mu);
     GB_Obj *w = g_pend.w, *m = g_pend.mask;
+    if (w && w->magic == GB_MAGIC && m && m->magic == GB_MAGIC && w->invalid == GrB_SUCCESS) {
+        try {
+            // fault injection for the tests (knob inject_flush_fail = 1)
+            GB_REQUIRE(gb_knob("inject_flush_fail") != 1, GrB_OUT_OF_MEMORY, "injected failure");
+            assign_all_scalar_fast(w, m, g_pend.x, g_pend.d);
+        } catch (const gb_exception &e) {
+            w->invalid = e.info;
+            w->err = "deferred GrB_Vector_assign failed: " + e.msg;
+        } catch (const std::bad_alloc &) {
+            w->invalid = GrB_OUT_OF_MEMORY;
+            w->err = "deferred GrB_Vector_assign failed: out of host memory";
+        }
+    }
     g_pend.w = g_pend.mask = nullptr;
     g_pending_active.store(false, std::memory_order_release);
-    if (w && w->magic == GB_MAGIC && m && m->magic == GB_MAGIC) assign_all_scalar_fast(w, m, g_pend.x, g_pend.d);
 }
 
 static bool try_defer_assign(GB_Obj *w, GB_Obj *mask, const char *xc, const gb_desc &d) {

@@ -16,16 +16,48 @@ static inline unsigned gb_grid(int64_t n, int per_block = GB_BLOCK) {
 }
 
 // ------------------------------------------------------------------ scans / sorts
-void gb_exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n) {
-    // out has n+1 slots: out[0] = 0, out[i+1] = in[0] + ... + in[i]
+// out[0..len) += *carry (the previous chunk's last prefix, already final on the stream)
+__global__ void k_add_carry(int64_t *__restrict__ out, int64_t len, const int64_t *__restrict__ carry) {
+    const int64_t c = *carry;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < len; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] += c;
+}
+
+struct gb_u8_to_i64 {
+    __host__ __device__ int64_t operator()(uint8_t x) const { return (int64_t)x; }
+};
+
+// Inclusive sums into out[1..n] in chunks of < 2^31 items (hipCUB's item count is an
+// int); chunk c > 0 then adds out[start_c], the previous chunk's total.
+template <class It>
+static void scan_chunked(It in, int64_t *out, int64_t n) {
     gb_memset(out, 0, sizeof(int64_t));
     if (n == 0) return;
-    GB_REQUIRE(n < (1LL << 31), GrB_NOT_IMPLEMENTED, "scan of more than 2^31 items");
+    const int64_t CH = (int64_t)1 << 30;
     size_t tmp = 0;
-    GB_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tmp, in, out + 1, (int)n, gb_stream()));
+    GB_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tmp, in, out + 1, (int)std::min(n, CH), gb_stream()));
     void *t = gb_malloc(tmp);
-    GB_HIP(hipcub::DeviceScan::InclusiveSum(t, tmp, in, out + 1, (int)n, gb_stream()));
+    for (int64_t off = 0; off < n; off += CH) {
+        const int64_t len = std::min(n - off, CH);
+        size_t tb = tmp;
+        GB_HIP(hipcub::DeviceScan::InclusiveSum(t, tb, in + off, out + 1 + off, (int)len, gb_stream()));
+        if (off) {
+            hipLaunchKernelGGL(k_add_carry, dim3(gb_grid(len, GB_BLOCK * 8)), dim3(GB_BLOCK), 0, gb_stream(),
+                               out + 1 + off, len, out + off);
+            GB_LAUNCH_CHECK();
+        }
+    }
     gb_free(t);
+}
+
+void gb_exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n) {
+    // out has n+1 slots: out[0] = 0, out[i+1] = in[0] + ... + in[i]; any n (chunked)
+    scan_chunked(in, out, n);
+}
+
+void gb_exclusive_scan_u8(const uint8_t *in, int64_t *out, int64_t n) {
+    // as gb_exclusive_scan_i64 over 0/1 byte flags, summed in int64
+    scan_chunked(hipcub::TransformInputIterator<int64_t, gb_u8_to_i64, const uint8_t *>(in, gb_u8_to_i64()), out, n);
 }
 
 __global__ void k_iota(int64_t *x, int64_t n) {

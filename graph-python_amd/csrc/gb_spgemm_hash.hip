@@ -808,7 +808,9 @@ void gb_spgemm_hash(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, GrB_Semiri
                 // symbolic: 2^19-column bitmap windows (64 KB); numeric: 2^17 columns (bitmap + word
                 // prefixes 32 KB) with values in LDS in groups of < 8192 entries (64 KB for 8-byte
                 // values; one-to-two-byte values: a group can hold the whole window)
-                const int lw = SYM ? win_log(19) : (sizeof(Z) < 4 ? win_log(13) : win_log(17));
+                // narrow values: at least 512 columns, so a value group (vcap - 256 entries,
+                // one 256-column chunk of headroom) is never empty
+                const int lw = SYM ? win_log(19) : (sizeof(Z) < 4 ? std::max(9, win_log(13)) : win_log(17));
                 int vcap = (SYM || !VALS) ? 0 : (sizeof(Z) < 4 ? (1 << lw) : 8192);
                 // tests: a small LDS value capacity sends windows to the C-resident accumulation
                 const int64_t kv = gb_knob("window_vcap");

@@ -271,7 +271,7 @@ bool gb_writeback_vector(GB_Obj *C, gb_vec_result &T, GB_Obj *M, const gb_desc &
 // Entry-parallel merge of C and T under the mask (one thread per stored entry,
 // so R-MAT hub rows with 10^4-10^5 entries do not serialise a thread):
 //   1. flag every entry of C and of T that survives (k_merge_flag_c / _t);
-//   2. exclusive scans of both flag arrays (sc, st);
+//   2. exclusive scans of both (byte) flag arrays into int64 offsets (sc, st);
 //   3. row r of the output starts at sc[crp[r]] + st[trp[r]];
 //   4. a surviving C entry (r, j) lands at sc[e] + st[lower_bound of j in T's row r],
 //      a surviving T entry at st[e] + sc[lower_bound of j in C's row r]
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(WB_BLOCK) void k_merge_flag_c(
     int64_t nrows, int64_t cnz, const int64_t *__restrict__ crp, const int32_t *__restrict__ cci,
     const int64_t *__restrict__ trp, const int32_t *__restrict__ tci, const int64_t *__restrict__ mrp,
     const int32_t *__restrict__ mci, bool has_mask, bool mcomp, bool replace, bool accum,
-    int64_t *__restrict__ flag) {
+    uint8_t *__restrict__ flag) {
     WB_STRIDE(e, cnz) {
         const int64_t r = wb_row_of(crp, nrows, e);
         const int32_t j = cci[e];
@@ -331,7 +331,7 @@ __global__ __launch_bounds__(WB_BLOCK) void k_merge_flag_c(
 __global__ __launch_bounds__(WB_BLOCK) void k_merge_flag_t(
     int64_t nrows, int64_t tnz, const int64_t *__restrict__ trp, const int32_t *__restrict__ tci,
     const int64_t *__restrict__ mrp, const int32_t *__restrict__ mci, bool has_mask, bool mcomp, bool within_mask,
-    int64_t *__restrict__ flag) {
+    uint8_t *__restrict__ flag) {
     WB_STRIDE(e, tnz) {
         bool keep = true;
         if (!within_mask) {
@@ -428,8 +428,9 @@ void gb_writeback_matrix(GB_Obj *C, gb_mat_result &T, GB_Obj *M, const gb_desc &
     cast_mat_result(T, wcode);
     const bool has_mask = mask.present;
     const int64_t cnz = cv.nvals, tnz = T.nvals;
-    int64_t *fc = s.get<int64_t>(std::max<int64_t>(cnz, 1));
-    int64_t *ft = s.get<int64_t>(std::max<int64_t>(tnz, 1));
+    // 0/1 byte flags (scratch: 1 + 8 bytes per entry; the scans run in < 2^31-item chunks)
+    uint8_t *fc = s.get<uint8_t>(std::max<int64_t>(cnz, 1));
+    uint8_t *ft = s.get<uint8_t>(std::max<int64_t>(tnz, 1));
     int64_t *sc = s.get<int64_t>(cnz + 1);
     int64_t *st = s.get<int64_t>(tnz + 1);
     if (cnz)
@@ -441,8 +442,8 @@ void gb_writeback_matrix(GB_Obj *C, gb_mat_result &T, GB_Obj *M, const gb_desc &
                            T.colidx, mask.rowptr, mask.colidx, has_mask, mask.comp,
                            T.within_mask && has_mask && !mask.comp, ft);
     GB_LAUNCH_CHECK();
-    gb_exclusive_scan_i64(fc, sc, cnz);
-    gb_exclusive_scan_i64(ft, st, tnz);
+    gb_exclusive_scan_u8(fc, sc, cnz);
+    gb_exclusive_scan_u8(ft, st, tnz);
     int64_t *orp = gb_malloc_n<int64_t>(nrows + 1);
     hipLaunchKernelGGL(k_merge_rowptr, dim3(wb_grid(nrows + 1)), dim3(WB_BLOCK), 0, gb_stream(), nrows, cv.rowptr,
                        T.rowptr, sc, st, orp);

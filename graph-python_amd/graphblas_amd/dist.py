@@ -57,55 +57,75 @@ class RowPanelAllGather:
     (SURVEY §8(e) mxm row).
 
     Rank k holds rows [lo_k, hi_k) of B as a local CSR -- rowptr int64[nr_k+1] from 0,
-    colidx int32[nnz_k], values [nnz_k] (or [1] when every panel is iso with one value) --
-    and the blocks follow rank order.  run() returns the whole B (rowptr int64[n+1],
-    colidx, values) on every rank.  RCCL has no gatherv: the panel sizes are all-gathered
-    first (two int64 per rank), then each owner broadcasts its panel straight into its
-    slice of the assembled buffers (no padding to the largest panel, no staging copy; on
-    the xGMI mesh every GPU receives each peer's panel over the direct link) and the local
-    row pointers are shifted by the panel's entry offset.  Issued on the library stream,
-    the result feeds GxB_Matrix_import_device."""
+    colidx int32[nnz_k], values [nnz_k] (or [1] when the panel is iso) -- and the blocks
+    follow rank order.  run() returns the whole B (rowptr int64[n+1], colidx, values,
+    iso) on every rank.  RCCL has no gatherv: the panel sizes, iso flags and iso values
+    are all-gathered first (four int64 per rank), then each owner broadcasts its panel
+    straight into its slice of the assembled buffers (no padding to the largest panel, no
+    staging copy; on the xGMI mesh every GPU receives each peer's panel over the direct
+    link) and the local row pointers are shifted by the panel's entry offset.  The result
+    is iso only when every panel is iso with the same value; otherwise iso panels are
+    expanded into their slice, so every rank issues the same collective sequence.  Issued
+    on the library stream, the result feeds GxB_Matrix_import_device."""
 
     def __init__(self, dist, world, rank):
         self.dist, self.world, self.rank = dist, world, rank
 
-    def sizes(self, nr, nnz, device):
+    @staticmethod
+    def _value_bits(values):
+        """The first value's bytes as one int64 (zero-padded), for the iso agreement check."""
         import torch
 
-        meta = torch.tensor([nr, nnz], dtype=torch.int64, device=device)
+        raw = values[:1].contiguous().cpu().view(torch.uint8).numpy().tobytes()
+        return int.from_bytes(raw[:8].ljust(8, b"\0"), "little", signed=True)
+
+    def sizes(self, nr, nnz, device, iso=False, iso_bits=0):
+        """[(nrows, nnz, iso, iso value bits)] of every rank, in rank order."""
+        import torch
+
+        meta = torch.tensor([nr, nnz, int(bool(iso)), iso_bits], dtype=torch.int64, device=device)
         got = [torch.zeros_like(meta) for _ in range(self.world)]
         self.dist.all_gather(got, meta)
-        return [(int(t[0]), int(t[1])) for t in torch.stack(got).cpu()]
+        return [tuple(int(x) for x in t) for t in torch.stack(got).cpu()]
 
     def run(self, rowptr, colidx, values, iso=False):
         import torch
 
         W, r = self.world, self.rank
         dev = rowptr.device
-        sz = self.sizes(rowptr.numel() - 1, colidx.numel(), dev)
+        bits = self._value_bits(values) if iso and values.numel() else 0
+        sz = self.sizes(rowptr.numel() - 1, colidx.numel(), dev, iso, bits)
+        # iso result only when all panels agree (value bits compared exactly)
+        all_iso = all(s[2] for s in sz) and len({s[3] for s in sz}) == 1
         roff, eoff = [0], [0]
-        for nr, nz in sz:
-            roff.append(roff[-1] + nr)
-            eoff.append(eoff[-1] + nz)
+        for s in sz:
+            roff.append(roff[-1] + s[0])
+            eoff.append(eoff[-1] + s[1])
         out_rp = torch.zeros(roff[-1] + 1, dtype=torch.int64, device=dev)
         out_ci = torch.empty(eoff[-1], dtype=colidx.dtype, device=dev)
-        out_vx = values.clone() if iso else torch.empty(eoff[-1], dtype=values.dtype, device=dev)
+        if all_iso:
+            out_vx = values[:1].clone()
+        else:
+            out_vx = torch.empty(eoff[-1], dtype=values.dtype, device=dev)
+            mine = out_vx[eoff[r]:eoff[r + 1]]
+            if iso:
+                mine.copy_(values[:1].expand(mine.numel()))
+            else:
+                mine.copy_(values)
         out_rp[roff[r] + 1:roff[r + 1] + 1].copy_(rowptr[1:])
         out_ci[eoff[r]:eoff[r + 1]].copy_(colidx)
-        if not iso:
-            out_vx[eoff[r]:eoff[r + 1]].copy_(values)
         if W > 1:
             for k in range(W):
                 if sz[k][0]:
                     self.dist.broadcast(out_rp[roff[k] + 1:roff[k + 1] + 1], src=k)
                 if sz[k][1]:
                     self.dist.broadcast(out_ci[eoff[k]:eoff[k + 1]], src=k)
-                    if not iso:
+                    if not all_iso:
                         self.dist.broadcast(out_vx[eoff[k]:eoff[k + 1]], src=k)
         for k in range(W):
             if sz[k][0] and eoff[k]:
                 out_rp[roff[k] + 1:roff[k + 1] + 1] += eoff[k]
-        return out_rp, out_ci, out_vx
+        return out_rp, out_ci, out_vx, all_iso
 
 
 _TYPESTR = {0: "|b1", 1: "|i1", 2: "|u1", 3: "<i2", 4: "<u2", 5: "<i4", 6: "<u4", 7: "<i8", 8: "<u8",
@@ -126,7 +146,7 @@ def gather_row_panels(lib, torch, gatherer, A, ncols):
     rp = gdev.device_tensor(torch, v.rowptr, v.nrows + 1)
     ci = gdev.device_tensor(torch, v.colidx, v.nvals, "<i4")
     vx = gdev.device_tensor(torch, v.values, 1 if v.iso else v.nvals, _TYPESTR[v.type_code])
-    brp, bci, bvx = gatherer.run(rp, ci, vx, iso=bool(v.iso))
+    brp, bci, bvx, biso = gatherer.run(rp, ci, vx, iso=bool(v.iso))
     tp = ctypes.c_void_p()
     rc = lib.GxB_Matrix_type(ctypes.byref(tp), A)
     if rc != 0:
@@ -134,7 +154,7 @@ def gather_row_panels(lib, torch, gatherer, A, ncols):
     B = ctypes.c_void_p()
     rc = lib.GxB_Matrix_import_device(ctypes.byref(B), tp, brp.numel() - 1, ncols, ctypes.c_void_p(brp.data_ptr()),
                                       ctypes.c_void_p(bci.data_ptr()), ctypes.c_void_p(bvx.data_ptr()),
-                                      bci.numel(), bool(v.iso))
+                                      bci.numel(), bool(biso))
     if rc != 0:
         raise RuntimeError(f"GxB_Matrix_import_device failed: {rc}")
     return B, brp

@@ -36,7 +36,8 @@ def _worker(rank, world, port, scale, ef, out_q):
     rp = torch.from_numpy(G.indptr[lo:hi + 1] - p0)
     ci = torch.from_numpy(G.indices[p0:p1].astype(np.int32))
     vx = torch.from_numpy(G.values[p0:p1].copy())
-    brp, bci, bvx = gdist.RowPanelAllGather(dist, world, rank).run(rp, ci, vx)
+    brp, bci, bvx, biso = gdist.RowPanelAllGather(dist, world, rank).run(rp, ci, vx)
+    assert not biso
     B = O.Csr(n, n, "FP64", brp.numpy(), bci.numpy(), bvx.numpy())
     Ar = O.Csr(hi - lo, n, "FP64", rp.numpy(), ci.numpy(), vx.numpy())
     C = O.mxm(O.Csr.empty(hi - lo, n, "FP64"), Ar, B, ("PLUS", "TIMES", "FP64"))
@@ -91,9 +92,67 @@ def test_row_panel_world1_and_iso():
     rp = torch.from_numpy(G.indptr.copy())
     ci = torch.from_numpy(G.indices.astype(np.int32))
     vx = torch.from_numpy(G.values.copy())
-    brp, bci, bvx = gdist.RowPanelAllGather(_One(), 1, 0).run(rp, ci, vx)
+    brp, bci, bvx, biso = gdist.RowPanelAllGather(_One(), 1, 0).run(rp, ci, vx)
+    assert not biso
     assert np.array_equal(brp.numpy(), G.indptr) and np.array_equal(bci.numpy(), ci.numpy())
     assert np.array_equal(bvx.numpy(), G.values)
     one = torch.ones(1, dtype=torch.float64)
-    _, _, ivx = gdist.RowPanelAllGather(_One(), 1, 0).run(rp, ci, one, iso=True)
-    assert ivx.numel() == 1 and float(ivx[0]) == 1.0
+    _, _, ivx, iiso = gdist.RowPanelAllGather(_One(), 1, 0).run(rp, ci, one, iso=True)
+    assert iiso and ivx.numel() == 1 and float(ivx[0]) == 1.0
+
+
+def _iso_worker(rank, world, port, kinds, out_q):
+    """rank r's panel: rows [lo, hi) of a fixed R-MAT pattern with values per kinds[r]:
+    ("iso", v) -> one value v, ("full", None) -> its own values."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    G = O.rmat(7, 8, 42, values="FP64", value_seed=2)
+    part = gdist.partition(G.nrows, world, rank)
+    lo, hi = part["lo"], part["hi"]
+    p0, p1 = int(G.indptr[lo]), int(G.indptr[hi])
+    rp = torch.from_numpy(G.indptr[lo:hi + 1] - p0)
+    ci = torch.from_numpy(G.indices[p0:p1].astype(np.int32))
+    kind, val = kinds[rank]
+    if kind == "iso":
+        vx, iso = torch.tensor([val], dtype=torch.float64), True
+    else:
+        vx, iso = torch.from_numpy(G.values[p0:p1].copy()), False
+    brp, bci, bvx, biso = gdist.RowPanelAllGather(dist, world, rank).run(rp, ci, vx, iso=iso)
+    out_q.put((rank, brp.numpy(), bci.numpy(), bvx.numpy(), biso))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kinds", [
+    [("iso", 3.0), ("full", None)],       # mixed: iso panel expanded, no collective mismatch
+    [("iso", 3.0), ("iso", 5.0)],         # all iso, different values: expanded per panel
+    [("iso", 2.5), ("iso", 2.5)],         # all iso, same value: iso result
+])
+def test_row_panel_mixed_iso(kinds):
+    """every rank must issue the same collective sequence and the assembled
+    values must be each panel's own (iso panels expanded unless all agree)."""
+    world = len(kinds)
+    G = O.rmat(7, 8, 42, values="FP64", value_seed=2)
+    expect = np.empty(G.nvals)
+    for r, (kind, val) in enumerate(kinds):
+        part = gdist.partition(G.nrows, world, r)
+        p0, p1 = int(G.indptr[part["lo"]]), int(G.indptr[part["hi"]])
+        expect[p0:p1] = val if kind == "iso" else G.values[p0:p1]
+    all_same_iso = all(k == "iso" for k, _ in kinds) and len({v for _, v in kinds}) == 1
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_iso_worker, args=(r, world, port, kinds, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, brp, bci, bvx, biso in res:
+        assert np.array_equal(brp, G.indptr) and np.array_equal(bci.astype(np.int64), G.indices)
+        assert biso == all_same_iso
+        if biso:
+            assert bvx.size == 1 and bvx[0] == kinds[0][1]
+        else:
+            assert np.array_equal(bvx, expect)

@@ -766,3 +766,24 @@ def test_deferred_assign_is_unobservable(gb):
             assert np.array_equal(x[0], y[0]) and np.array_equal(x[1], y[1])
         else:
             assert np.array_equal(np.asarray(x), np.asarray(y))
+
+
+def test_deferred_assign_failure_is_recorded_on_its_vector(gb):
+    """a failing deferred assign (injected) is an execution error of the
+    deferred vector -- the unrelated call that triggers the flush succeeds, and the
+    vector reports GrB_INVALID_OBJECT from then on."""
+    from graphblas_amd import exceptions as ex
+
+    n = 300
+    v = gb.Vector(gb.INT32, n)
+    q = gb.Vector.from_coo([1, 5, 9], True, dtype=bool, size=n)
+    other = gb.Vector.from_coo([2, 3], [1, 2], dtype=gb.INT64, size=n)
+    v(mask=q.V)[:] = 5  # deferred
+    gb.set_knob("inject_flush_fail", 1)
+    try:
+        assert other.nvals == 2  # triggers the flush; the failure is not this call's
+    finally:
+        gb.set_knob("inject_flush_fail", 0)
+    with pytest.raises(ex.InvalidObject):
+        v.nvals
+    assert q.nvals == 3 and other.nvals == 2
