@@ -321,6 +321,23 @@ GB_HD T gb_monoid(int m, T x, T y) {
     }
 }
 
+// identity of a monoid on T (ANY has none: callers store its first value instead)
+template <class T>
+GB_HD T gb_monoid_identity(int m) {
+    switch (m) {
+    case GBAMD_MON_TIMES: return (T)1;
+    case GBAMD_MON_MIN: return gb_tmax<T>();
+    case GBAMD_MON_MAX: return gb_tmin<T>();
+    case GBAMD_MON_LAND: return (T)1;
+    case GBAMD_MON_LXNOR: return (T)1;
+    case GBAMD_MON_BAND:
+    case GBAMD_MON_BXNOR:
+        if constexpr (gb_traits<T>::is_int) return (T)~(T)0;
+        else return (T)1;
+    default: return (T)0;  // PLUS, LOR, LXOR, BOR, BXOR
+    }
+}
+
 // terminal value of a monoid: once reached, further terms cannot change it
 template <class T>
 GB_HD bool gb_monoid_terminal(int m, T z) {
@@ -395,6 +412,13 @@ struct gb_sr_lor_land {
 // ------------------------------------------------------------------ wave helpers
 GB_DEV int gb_lane() { return __lane_id(); }
 
+// LDS written by some lanes of a wave, read by others: order the wave's accesses
+GB_DEV void gb_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <class T>
 GB_DEV T gb_shfl_xor(T v, int mask, int width) {
     if constexpr (sizeof(T) == 8) {
@@ -417,6 +441,28 @@ GB_DEV T gb_shfl_xor(T v, int mask, int width) {
         int x = 0;
         __builtin_memcpy(&x, &v, sizeof(T));
         x = __shfl_xor(x, mask, width);
+        T r;
+        __builtin_memcpy(&r, &x, sizeof(T));
+        return r;
+    }
+}
+
+// read v from lane src (any lane pattern: ds_bpermute), any type up to 8 bytes
+template <class T>
+GB_DEV T gb_shfl(T v, int src, int width = 64) {
+    if constexpr (sizeof(T) == 8) {
+        int64_t x;
+        __builtin_memcpy(&x, &v, 8);
+        int lo = __shfl((int)(x & 0xffffffff), src, width);
+        int hi = __shfl((int)(x >> 32), src, width);
+        int64_t y = ((int64_t)(uint32_t)lo) | ((int64_t)hi << 32);
+        T r;
+        __builtin_memcpy(&r, &y, 8);
+        return r;
+    } else {
+        int x = 0;
+        __builtin_memcpy(&x, &v, sizeof(T));
+        x = __shfl(x, src, width);
         T r;
         __builtin_memcpy(&r, &x, sizeof(T));
         return r;

@@ -1,0 +1,586 @@
+// gb_dot.hip -- masked dot-product SpGEMM, two-sided LDS method: the kernel
+// behind GrB_mxm with a non-complemented mask (replaces SuiteSparse's
+// GB_AxB_dot3, reached from reference core/matrix.py:2241 via core/base.py:483)
+// for monoids whose fold order cannot change the result (exact_monoid in
+// gb_mxm.hip: min/max on integers, integer plus/times, logical/bitwise, any_pair).
+//
+// T(i,j) for (i,j) in M intersects the sorted lists A'(i,:) and B'^T(j,:).  The
+// cost of an intersection is set by the shorter list when the longer one can be
+// searched cheaply, and the longer list is shared by every mask entry of its row
+// (A' side) or column (B'^T side).  So every mask entry is given to the side
+// that owns its longer list:
+//   phase R: entries with |A'(i,:)| >= |B'^T(j,:)|, grouped by mask row i
+//            (the mask's CSR);
+//   phase C: entries with |B'^T(j,:)| > |A'(i,:)|, grouped by mask column j
+//            (the mask's CSC, whose position map gives each entry's CSR slot).
+// Per group g (row or column) the longer list X(g,:) is loaded once; each
+// entry's shorter list Y(o,:) is streamed (coalesced) and every key is searched
+// in X(g,:):
+//   * |X(g,:)| <= 64: a wave per group, X's keys and values held one per lane,
+//     membership by a 6-step shuffle search (k_dot_small);
+//   * |X(g,:)| <= 16384: a workgroup per task, X's keys in LDS (64 KB) behind a
+//     hashed membership bitmap (32 KB: one LDS read rejects most keys), binary
+//     search for the rest; tasks are runs of one group's entries cut at fixed
+//     windows of streamed work (<= 256 entries), so R-MAT hub rows are spread over
+//     many workgroups; one flat stream over the task's entries keeps every lane
+//     busy for short and long Y lists alike (k_dot_task);
+//   * longer (R-MAT's largest hubs): the per-entry wave kernel of gb_mxm.hip.
+// Work is sum over mask entries of min(|A'(i,:)|, |B'^T(j,:)|) streamed keys
+// plus one LDS search each -- instead of a search in global memory per key.
+#include <algorithm>
+
+#include "gb_dispatch.cuh"
+#include "gb_internal.h"
+
+namespace {
+
+constexpr int DT_BLOCK = 256;
+constexpr int DT_SMALL = 64;      // long side <= 64: k_dot_small, keys one per lane
+constexpr int DT_MID = 256;       // long side <= 256: k_dot_small, four keys per lane
+constexpr int DT_CAP = 16384;     // long side <= DT_CAP: k_dot_task (keys in LDS)
+constexpr int DT_OVH = 256;       // per-entry cost added to the streamed length (task windows)
+constexpr int DT_WIN = 65536;     // task window: <= DT_WIN / DT_OVH entries start in one
+constexpr int DT_MAXE = DT_WIN / DT_OVH;
+
+static inline unsigned dt_grid(int64_t n, int per_block = DT_BLOCK, int64_t cap = 1 << 16) {
+    int64_t g = (n + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+
+// one phase's view: groups (rows of the mask for R, its columns for C), the
+// longer lists X (indexed by group) and the shorter lists Y (indexed by the
+// entry's other index)
+struct dt_side {
+    const int64_t *grp_rp;  // [ng+1] entries of group g: [grp_rp[g], grp_rp[g+1])
+    const int32_t *grp_oi;  // [nm]   other index of each entry
+    const int64_t *perm;    // [nm]   entry -> CSR position of the mask (nullptr: identity)
+    int64_t ng;
+    const int64_t *xrp;
+    const int32_t *xci;
+    const int64_t *yrp;
+    const int32_t *yci;
+};
+
+// the entry belongs to this phase: R takes |X| >= |Y|, C takes |X| > |Y|
+template <bool SWAP>
+__device__ __forceinline__ bool dt_side_of(int64_t a, int64_t b) {
+    return SWAP ? a > b : a >= b;
+}
+
+// ---------------------------------------------------------------- classify
+// flags (pre-zeroed): tflag[p] = 1 for this phase's entries of task-sized groups
+// (G order); hflag[q] = 1 for entries whose longer list exceeds DT_CAP (CSR order)
+template <bool SWAP>
+__global__ __launch_bounds__(DT_BLOCK) void k_dt_classify(dt_side s, int cap, uint8_t *__restrict__ tflag,
+                                                         uint8_t *__restrict__ hflag) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t g = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; g < s.ng; g += nw) {
+        const int64_t a = s.xrp[g + 1] - s.xrp[g];
+        if (a <= DT_MID) continue;  // k_dot_small (or nothing to match)
+        for (int64_t p = s.grp_rp[g] + lane; p < s.grp_rp[g + 1]; p += 64) {
+            const int32_t o = s.grp_oi[p];
+            const int64_t b = s.yrp[o + 1] - s.yrp[o];
+            if (!dt_side_of<SWAP>(a, b)) continue;
+            if (a <= cap) tflag[p] = 1;
+            else hflag[s.perm ? s.perm[p] : p] = 1;
+        }
+    }
+}
+
+// compacted task entries in G order: group, Y start and length, other index, CSR slot
+template <bool SWAP>
+__global__ __launch_bounds__(DT_BLOCK) void k_dt_compact(dt_side s, int cap, const uint8_t *__restrict__ tflag,
+                                                        const int64_t *__restrict__ pos, int32_t *__restrict__ eG,
+                                                        int64_t *__restrict__ eYS, int32_t *__restrict__ eO,
+                                                        int32_t *__restrict__ eB, int64_t *__restrict__ eQ) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t g = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; g < s.ng; g += nw) {
+        const int64_t a = s.xrp[g + 1] - s.xrp[g];
+        if (a <= DT_MID || a > cap) continue;
+        for (int64_t p = s.grp_rp[g] + lane; p < s.grp_rp[g + 1]; p += 64) {
+            if (!tflag[p]) continue;
+            const int32_t o = s.grp_oi[p];
+            const int64_t e = pos[p];
+            const int64_t ys = s.yrp[o];
+            eG[e] = (int32_t)g;
+            eYS[e] = ys;
+            eO[e] = o;
+            eB[e] = (int32_t)(s.yrp[o + 1] - ys);
+            eQ[e] = s.perm ? s.perm[p] : p;
+        }
+    }
+}
+
+// a task starts where the group changes or the cost prefix enters a new window
+__global__ void k_dt_task_flags(int64_t ne, int64_t win, const int32_t *__restrict__ eG,
+                                const int64_t *__restrict__ cum, uint8_t *__restrict__ ts) {
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x)
+        ts[e] = (e == 0 || eG[e] != eG[e - 1] || cum[e] / win != cum[e - 1] / win) ? 1 : 0;
+}
+
+__global__ void k_dt_task_fill(int64_t ne, const uint8_t *__restrict__ ts, const int64_t *__restrict__ tpos,
+                               int64_t *__restrict__ tstart) {
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x)
+        if (ts[e]) tstart[tpos[e]] = e;
+    if (blockIdx.x == 0 && threadIdx.x == 0) tstart[tpos[ne]] = ne;
+}
+
+__global__ void k_dt_positions(int64_t n, const uint8_t *__restrict__ flag, const int64_t *__restrict__ pos,
+                               int64_t *__restrict__ out) {
+    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x)
+        if (flag[q]) out[pos[q]] = q;
+}
+
+// ---------------------------------------------------------------- folds
+// fold z into a 64-bit LDS slot holding a Z (monoid with identity; exact, so any
+// arrival order gives the same result)
+template <class SR, class Z>
+__device__ __forceinline__ void dt_lds_fold(const SR &sr, unsigned long long *slot, Z z) {
+    if constexpr (std::is_same<SR, gb_sr_min_plus<int64_t>>::value) {
+        atomicMin((long long *)slot, (long long)z);
+    } else if constexpr (std::is_same<SR, gb_sr_plus_times<int64_t>>::value) {
+        atomicAdd(slot, (unsigned long long)z);
+    } else {
+        unsigned long long old = *(volatile unsigned long long *)slot;
+        while (true) {
+            Z cur;
+            __builtin_memcpy(&cur, &old, sizeof(Z));
+            const Z nv = sr.add(cur, z);
+            unsigned long long nb = old;
+            __builtin_memcpy(&nb, &nv, sizeof(Z));
+            if (nb == old) return;
+            const unsigned long long prev = atomicCAS(slot, old, nb);
+            if (prev == old) return;
+            old = prev;
+        }
+    }
+}
+
+// wave fold of (found, acc) into every lane (butterfly; exact monoids)
+template <class SR, class Z>
+__device__ __forceinline__ void dt_wave_fold(const SR &sr, bool &found, Z &acc) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const bool of = __shfl_xor((int)found, off, 64);
+        const Z oz = gb_shfl_xor(acc, off, 64);
+        if (of) {
+            acc = found ? sr.add(acc, oz) : oz;
+            found = true;
+        }
+    }
+}
+
+template <class SR, class X, class Z, bool SWAP>
+__device__ __forceinline__ Z dt_mult(const SR &sr, X xv, X yv, int64_t g, int32_t k, int64_t o) {
+    // R: x = A'(i,k), y = B'(k,j), i = g, j = o;  C: x = B'(k,j), y = A'(i,k), i = o, j = g
+    if constexpr (SWAP) return sr.mult(yv, xv, o, k, g);
+    else return sr.mult(xv, yv, g, k, o);
+}
+
+// ---------------------------------------------------------------- small groups
+// a wave per group with 1 <= |X(g,:)| <= 64*KPL: lane l holds X's keys
+// [l*KPL, l*KPL + KPL) (and, for KPL = 1, its value); the group's entries are read
+// 64 at a time (other index, Y bounds) and taken one after the other: lanes load
+// Y's keys 64 at a time (|Y| <= |X|) and find each among X's keys by shuffles --
+// 6 steps over the lanes' first keys, then the KPL keys of the lane found.
+template <class SR, class X, class Z, bool SWAP, int KPL>
+__global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, dt_side s, const X *__restrict__ xvx, bool x_iso,
+                                                       const X *__restrict__ yvx, bool y_iso,
+                                                       Z *__restrict__ tval, uint8_t *__restrict__ tflag) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const bool rv = SR::reads_values && xvx && yvx;
+    constexpr int AMIN = KPL == 1 ? 1 : DT_SMALL + 1;
+    for (int64_t g = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; g < s.ng; g += nw) {
+        const int64_t xs = s.xrp[g];
+        const int a = __builtin_amdgcn_readfirstlane((int)(s.xrp[g + 1] - xs));
+        const int64_t p0 = s.grp_rp[g], p1 = s.grp_rp[g + 1];
+        const int cnt_e = __builtin_amdgcn_readfirstlane((int)(p1 - p0));
+        if (a < AMIN || a > 64 * KPL || cnt_e == 0) continue;  // before any cross-lane operation
+        int32_t xk[KPL];
+#pragma unroll
+        for (int j = 0; j < KPL; j++) xk[j] = lane * KPL + j < a ? s.xci[xs + lane * KPL + j] : 0x7fffffff;
+        X xv = X();
+        if (KPL == 1 && rv && lane < a) xv = xvx[x_iso ? 0 : xs + lane];
+        for (int64_t pb = p0; pb < p1; pb += 64) {
+            const int nb = __builtin_amdgcn_readfirstlane((int)std::min<int64_t>(64, p1 - pb));
+            int32_t o_l = 0;
+            int64_t ys_l = 0;
+            int b_l = 0;
+            if (lane < nb) {
+                o_l = s.grp_oi[pb + lane];
+                ys_l = s.yrp[o_l];
+                b_l = (int)(s.yrp[o_l + 1] - ys_l);
+            }
+            for (int t = 0; t < nb; t++) {
+                // (no `continue` in this loop: its body holds cross-lane operations)
+                const int b = __builtin_amdgcn_readlane(b_l, t);
+                if (b > 0 && dt_side_of<SWAP>(a, b)) {
+                    const int32_t o = __builtin_amdgcn_readlane(o_l, t);
+                    const int64_t ys = gb_shfl(ys_l, t);
+                    bool found = false;
+                    Z acc = Z();
+                    for (int f0 = 0; f0 < b; f0 += 64) {
+                        const bool act = f0 + lane < b;
+                        const int32_t yk = act ? s.yci[ys + f0 + lane] : -1;
+                        int pos = -1;
+                        X xm = X();
+                        if constexpr (KPL == 1) {
+                            int lo = 0;
+#pragma unroll
+                            for (int st = 32; st > 0; st >>= 1)
+                                if (__shfl(xk[0], lo + st - 1, 64) < yk) lo += st;
+                            // every lane takes part in the shuffle (a lane outside |Y| still serves its key)
+                            const int32_t xl = __shfl(xk[0], lo, 64);
+                            xm = gb_shfl(xv, lo);
+                            if (act && xl == yk) pos = lo;
+                        } else {
+                            int L = 0;  // last lane whose first key <= yk
+#pragma unroll
+                            for (int st = 32; st > 0; st >>= 1) {
+                                const int c = L + st;
+                                const int32_t v = __shfl(xk[0], c < 64 ? c : 63, 64);
+                                if (c < 64 && v <= yk) L = c;
+                            }
+#pragma unroll
+                            for (int j = 0; j < KPL; j++) {
+                                const int32_t v = __shfl(xk[j], L, 64);
+                                if (act && v == yk) pos = L * KPL + j;
+                            }
+                            if (rv && pos >= 0) xm = xvx[x_iso ? 0 : xs + pos];
+                        }
+                        if (pos >= 0) {
+                            X yv = X();
+                            if (rv) yv = yvx[y_iso ? 0 : ys + f0 + lane];
+                            const Z z = dt_mult<SR, X, Z, SWAP>(sr, xm, yv, g, yk, o);
+                            acc = found ? sr.add(acc, z) : z;
+                            found = true;
+                        }
+                    }
+                    if (__ballot(found)) {
+                        dt_wave_fold(sr, found, acc);
+                        if (lane == 0) {
+                            const int64_t p = pb + t;
+                            const int64_t q = s.perm ? s.perm[p] : p;
+                            tval[q] = acc;
+                            tflag[q] = 1;
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- task groups
+// A workgroup per task (a run of <= DT_MAXE entries of one group g with
+// 256 < |X(g,:)| <= DT_CAP); the entries' other index, Y bounds and output slot
+// come precomputed in task order (k_dt_compact).
+//  1. X(g,:)'s keys go to LDS as they are (sorted) plus a hashed membership filter
+//     (2^18 bits, <= 6.25 % set): one LDS read rejects most Y keys.
+//  2. Entries are cut into units of <= DT_PIECE elements of their Y list; waves
+//     take units from an LDS counter.  In a unit the wave streams Y's keys 64 lanes
+//     wide (coalesced), DT_U loads in flight per lane, filters them, packs the
+//     keys that pass (~hits + 6 %) densely into a per-wave LDS stage and binary-
+//     searches those in X's keys with every lane busy; hits load both values and
+//     fold in registers, one wave fold per unit.  A one-unit entry is written
+//     straight to T; a longer entry's units meet in an LDS slot (atomic fold of an
+//     exact monoid) written at the end of the task.
+constexpr int DT_TB = 1024;      // task workgroup: 16 waves, one workgroup per CU
+constexpr int DT_U = 4;          // Y keys in flight per lane
+constexpr int DT_PIECE = 1024;   // elements per unit
+constexpr int DT_MAXU = DT_MAXE + DT_WIN / DT_PIECE + DT_CAP / DT_PIECE + 2;  // units per task bound
+constexpr int DT_FLOG = 18;      // filter bits (log2)
+
+__device__ __forceinline__ uint32_t dt_hash(int32_t k) { return ((uint32_t)k * 0x9E3779B1u) >> (32 - DT_FLOG); }
+
+template <class SR, class X, class Z, bool SWAP>
+__global__ __launch_bounds__(DT_TB) void k_dot_task(
+    SR sr, int mon, dt_side s, const X *__restrict__ xvx, bool x_iso, const X *__restrict__ yvx, bool y_iso,
+    int64_t ntask, const int64_t *__restrict__ tstart, const int32_t *__restrict__ eG,
+    const int64_t *__restrict__ eYS, const int32_t *__restrict__ eO, const int32_t *__restrict__ eB,
+    const int64_t *__restrict__ eQ, Z *__restrict__ tval, uint8_t *__restrict__ tflag, int dbg) {
+    __shared__ int32_t keys[DT_CAP];
+    __shared__ uint32_t filt[1 << (DT_FLOG - 5)];
+    __shared__ int32_t stage_k[DT_TB / 64][64 * DT_U];
+    __shared__ int32_t stage_f[DT_TB / 64][64 * DT_U];
+    __shared__ int64_t e_ys[DT_MAXE];
+    __shared__ int64_t e_q[DT_MAXE];
+    __shared__ int32_t e_o[DT_MAXE];
+    __shared__ int32_t e_b[DT_MAXE];
+    __shared__ int32_t e_upre[DT_MAXE + 1];
+    __shared__ int16_t u2e[DT_MAXU];
+    __shared__ unsigned long long e_acc[DT_MAXE];
+    __shared__ int e_fnd[DT_MAXE];
+    __shared__ int w_sum[DT_TB / 64];
+    __shared__ int next_unit;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const bool rv = SR::reads_values && xvx && yvx;
+    // ANY (any_pair, or LOR over pair's 1s): the entry's value is any term -- store it;
+    // every other monoid folds into its identity
+    const bool ANY = std::is_same<SR, gb_sr_any_pair<Z>>::value || mon == GBAMD_MON_ANY;
+    const Z ident = ANY ? Z() : gb_monoid_identity<Z>(mon);
+    const unsigned long long ltmask = (1ULL << lane) - 1;
+    int32_t *stk = stage_k[wid];
+    int32_t *stf = stage_f[wid];
+    for (int64_t t = blockIdx.x; t < ntask; t += gridDim.x) {
+        const int64_t e0 = tstart[t];
+        const int ne = (int)(tstart[t + 1] - e0);
+        const int64_t g = eG[e0];
+        const int64_t xs = s.xrp[g];
+        const int a = (int)(s.xrp[g + 1] - xs);
+        for (int i = tid; i < (1 << (DT_FLOG - 5)); i += DT_TB) filt[i] = 0;
+        int nu = 0;
+        if (tid < ne) {
+            const int b = eB[e0 + tid];
+            e_ys[tid] = eYS[e0 + tid];
+            e_o[tid] = eO[e0 + tid];
+            e_b[tid] = b;
+            e_q[tid] = eQ[e0 + tid];
+            unsigned long long iv = 0;
+            __builtin_memcpy(&iv, &ident, sizeof(Z));
+            e_acc[tid] = iv;
+            e_fnd[tid] = 0;
+            nu = (b + DT_PIECE - 1) / DT_PIECE;
+        }
+        int inc = nu;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(inc, off, 64);
+            if (lane >= off) inc += y;
+        }
+        if (lane == 63) w_sum[wid] = inc;
+        if (tid == 0) next_unit = 0;
+        __syncthreads();  // filter cleared, unit counts visible
+        for (int i = tid; i < a; i += DT_TB) {
+            const int32_t k = s.xci[xs + i];
+            keys[i] = k;
+            const uint32_t h = dt_hash(k);
+            atomicOr(&filt[h >> 5], 1u << (h & 31));
+        }
+        int base = 0, NU = 0;
+        for (int w = 0; w < DT_TB / 64; w++) {
+            if (w < wid) base += w_sum[w];
+            NU += w_sum[w];
+        }
+        if (tid < ne) {
+            e_upre[tid] = base + inc - nu;
+            for (int u = base + inc - nu; u < base + inc; u++) u2e[u] = (int16_t)tid;
+        }
+        if (tid == 0) e_upre[ne] = NU;
+        __syncthreads();
+        int ksteps = 0;
+        while ((1 << ksteps) < a) ksteps++;
+        // units: wave-uniform bookkeeping kept in scalar registers (readlane), so the
+        // loop exit and the trip counts are scalar branches
+        int unit = 0;
+        if (lane == 0) unit = atomicAdd(&next_unit, 1);
+        unit = __builtin_amdgcn_readlane(unit, 0);
+        while (unit < NU) {
+            const int e = __builtin_amdgcn_readfirstlane((int)u2e[unit]);
+            const int64_t ys_v = e_ys[e];
+            const int64_t ys = ((int64_t)__builtin_amdgcn_readfirstlane((int)(ys_v >> 32)) << 32) |
+                               (uint32_t)__builtin_amdgcn_readfirstlane((int)ys_v);
+            const int b = __builtin_amdgcn_readfirstlane(e_b[e]);
+            const int o = __builtin_amdgcn_readfirstlane(e_o[e]);
+            const int u0 = (unit - __builtin_amdgcn_readfirstlane(e_upre[e])) * DT_PIECE;
+            const int u1 = min(u0 + DT_PIECE, b);
+            bool found = false;
+            Z acc = Z();
+            for (int f0 = u0; f0 < ((dbg & 8) ? u0 : u1); f0 += 64 * DT_U) {
+                int32_t k[DT_U];
+#pragma unroll
+                for (int u = 0; u < DT_U; u++) {
+                    const int f = f0 + u * 64 + lane;
+                    k[u] = f < u1 ? ((dbg & 4) ? f : s.yci[ys + f]) : -1;
+                }
+                // filter, then pack the keys that pass into the wave's stage
+                int cnt = 0;
+#pragma unroll
+                for (int u = 0; u < DT_U; u++) {
+                    const uint32_t h = dt_hash(k[u]);
+                    const bool c = !(dbg & 2) && f0 + u * 64 + lane < u1 && ((filt[h >> 5] >> (h & 31)) & 1u);
+                    const unsigned long long m = __ballot(c);
+                    if (c) {
+                        const int idx = cnt + __popcll(m & ltmask);
+                        stk[idx] = k[u];
+                        stf[idx] = f0 + u * 64 + lane;
+                    }
+                    cnt += __popcll(m);
+                }
+                gb_wave_sync();
+                for (int r = 0; r < cnt; r += 64) {
+                    const bool act = r + lane < cnt;
+                    const int32_t kk = act ? stk[r + lane] : -1;
+                    const int ff = act ? stf[r + lane] : 0;
+                    int l = 0;  // number of X keys < kk
+                    for (int st = ksteps - 1; st >= 0; st--) {
+                        const int c = l + (1 << st);
+                        if (c <= a && keys[c - 1] < kk) l = c;
+                    }
+                    if (act && !(dbg & 1) && l < a && keys[l] == kk) {
+                        X xv = X(), yv = X();
+                        if (rv) {
+                            xv = xvx[x_iso ? 0 : xs + l];
+                            yv = yvx[y_iso ? 0 : ys + ff];
+                        }
+                        const Z z = dt_mult<SR, X, Z, SWAP>(sr, xv, yv, g, kk, o);
+                        acc = found ? sr.add(acc, z) : z;
+                        found = true;
+                    }
+                }
+                gb_wave_sync();  // the stage is rewritten by the next step
+            }
+            if (__ballot(found)) {
+                dt_wave_fold(sr, found, acc);
+                if (lane == 0) {
+                    if (b <= DT_PIECE) {
+                        tval[e_q[e]] = acc;
+                        tflag[e_q[e]] = 1;
+                    } else {
+                        if (ANY) {
+                            unsigned long long v = 0;
+                            __builtin_memcpy(&v, &acc, sizeof(Z));
+                            e_acc[e] = v;
+                        } else {
+                            dt_lds_fold(sr, &e_acc[e], acc);
+                        }
+                        e_fnd[e] = 1;
+                    }
+                }
+            }
+            int nxt = 0;
+            if (lane == 0) nxt = atomicAdd(&next_unit, 1);
+            unit = __builtin_amdgcn_readlane(nxt, 0);
+        }
+        __syncthreads();
+        if (tid < ne && e_b[tid] > DT_PIECE && e_fnd[tid]) {
+            Z v;
+            const unsigned long long raw = e_acc[tid];
+            __builtin_memcpy(&v, &raw, sizeof(Z));
+            tval[e_q[tid]] = v;
+            tflag[e_q[tid]] = 1;
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+// C-ABI-free internal entry (gb_mxm.hip): the two phases over one mask; tval / tflag
+// are indexed by the mask's CSR positions (tflag pre-zeroed by the caller).  Returns
+// the CSR positions of the entries left to the per-entry kernel (longer list >
+// DT_CAP) in *huge (device, caller frees) and their count.
+int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &mask, const gb_sr_info &info,
+                         const void *av, const void *btv, void *tval, uint8_t *tflag, int64_t **huge) {
+    const int64_t nm = mask.nvals;
+    *huge = nullptr;
+    if (nm == 0) return 0;
+    gb_scratch s;
+    // the mask's CSC with each entry's CSR position: cached on the mask matrix, or built
+    const int64_t *mtrp, *mperm;
+    const int32_t *mtci;
+    int64_t *own_rp = nullptr, *own_perm = nullptr;
+    int32_t *own_ci = nullptr;
+    void *own_vx = nullptr;
+    if (mask.obj) {
+        gb_csr_view mt;
+        gb_get_csc(mt, mask.obj);
+        mtrp = mt.rowptr;
+        mtci = mt.colidx;
+        mperm = gb_csc_perm(mask.obj);
+    } else {
+        gb_transpose_csr(A.nrows, BT.nrows, nm, mask.rowptr, mask.colidx, nullptr, 1, false, &own_rp, &own_ci, &own_vx,
+                         &own_perm);
+        mtrp = own_rp;
+        mtci = own_ci;
+        mperm = own_perm;
+    }
+    // knobs dot_cap / dot_win (tests) shrink the LDS list cap and the task window
+    int cap = DT_CAP;
+    int64_t win = DT_WIN;
+    if (gb_knob("dot_cap") > DT_MID && gb_knob("dot_cap") < DT_CAP) cap = (int)gb_knob("dot_cap");
+    if (gb_knob("dot_win") >= DT_OVH && gb_knob("dot_win") < DT_WIN) win = gb_knob("dot_win");
+    uint8_t *hflag = s.get<uint8_t>(nm);
+    gb_memset(hflag, 0, nm);
+    uint8_t *tf = s.get<uint8_t>(nm);
+    int64_t *pos = s.get<int64_t>(nm + 1);
+    gb_dispatch_sr(info, [&](auto srf, auto x, auto z) {
+        using SRT = decltype(srf);
+        using X = decltype(x);
+        using Z = decltype(z);
+        auto phase = [&](auto swapc) {
+            constexpr bool SWAP = decltype(swapc)::value;
+            dt_side sd;
+            if (!SWAP) {
+                sd = dt_side{mask.rowptr, mask.colidx, nullptr, A.nrows, A.rowptr, A.colidx, BT.rowptr, BT.colidx};
+            } else {
+                sd = dt_side{mtrp, mtci, mperm, BT.nrows, BT.rowptr, BT.colidx, A.rowptr, A.colidx};
+            }
+            const X *xv = (const X *)(SWAP ? btv : av);
+            const X *yv = (const X *)(SWAP ? av : btv);
+            const bool xiso = SWAP ? BT.iso : A.iso, yiso = SWAP ? A.iso : BT.iso;
+            const unsigned gw = dt_grid(sd.ng * 64, DT_BLOCK, 1 << 15);
+            hipLaunchKernelGGL((k_dot_small<SRT, X, Z, SWAP, 1>), dim3(gw), dim3(DT_BLOCK), 0, gb_stream(), srf, sd,
+                               xv, xiso, yv, yiso, (Z *)tval, tflag);
+            const int64_t skip = gb_knob("dot_skip");  // diagnostics: 1 skips the mid kernel, 2 the task kernel
+            if (!(skip & 1))
+                hipLaunchKernelGGL((k_dot_small<SRT, X, Z, SWAP, DT_MID / 64>), dim3(gw), dim3(DT_BLOCK), 0,
+                                   gb_stream(), srf, sd, xv, xiso, yv, yiso, (Z *)tval, tflag);
+            gb_memset(tf, 0, nm);
+            hipLaunchKernelGGL((k_dt_classify<SWAP>), dim3(gw), dim3(DT_BLOCK), 0, gb_stream(), sd, cap, tf, hflag);
+            GB_LAUNCH_CHECK();
+            gb_exclusive_scan_u8(tf, pos, nm);
+            const int64_t ne = gb_read_i64(pos + nm);
+            if (ne == 0) return;
+            gb_scratch ts;
+            int32_t *eG = ts.get<int32_t>(ne);
+            int64_t *eYS = ts.get<int64_t>(ne);
+            int32_t *eO = ts.get<int32_t>(ne);
+            int32_t *eB = ts.get<int32_t>(ne);
+            int64_t *eQ = ts.get<int64_t>(ne);
+            hipLaunchKernelGGL((k_dt_compact<SWAP>), dim3(gw), dim3(DT_BLOCK), 0, gb_stream(), sd, cap, tf, pos, eG,
+                               eYS, eO, eB, eQ);
+            GB_LAUNCH_CHECK();
+            int64_t *cum = ts.get<int64_t>(ne + 1);
+            gb_exclusive_scan_i32(eB, DT_OVH, cum, ne);
+            uint8_t *tsf = ts.get<uint8_t>(ne);
+            hipLaunchKernelGGL(k_dt_task_flags, dim3(dt_grid(ne)), dim3(DT_BLOCK), 0, gb_stream(), ne, win, eG, cum,
+                               tsf);
+            int64_t *tpos = ts.get<int64_t>(ne + 1);
+            gb_exclusive_scan_u8(tsf, tpos, ne);
+            const int64_t nt = gb_read_i64(tpos + ne);
+            int64_t *tstart = ts.get<int64_t>(nt + 1);
+            hipLaunchKernelGGL(k_dt_task_fill, dim3(dt_grid(ne)), dim3(DT_BLOCK), 0, gb_stream(), ne, tsf, tpos,
+                               tstart);
+            GB_LAUNCH_CHECK();
+            // persistent workgroups: one per CU
+            const unsigned gt = (unsigned)std::min<int64_t>(nt, 1024);
+            if (!(skip & 2))
+            hipLaunchKernelGGL((k_dot_task<SRT, X, Z, SWAP>), dim3(gt), dim3(DT_TB), 0, gb_stream(), srf, info.mon,
+                               sd, xv, xiso, yv, yiso, nt, tstart, eG, eYS, eO, eB, eQ, (Z *)tval, tflag,
+                               (int)gb_knob("dot_dbg"));
+            GB_LAUNCH_CHECK();
+        };
+        phase(std::false_type{});
+        phase(std::true_type{});
+    });
+    // entries left to the per-entry kernel
+    gb_exclusive_scan_u8(hflag, pos, nm);
+    const int64_t nh = gb_read_i64(pos + nm);
+    if (nh) {
+        int64_t *hq = gb_malloc_n<int64_t>(nh);
+        hipLaunchKernelGGL(k_dt_positions, dim3(dt_grid(nm)), dim3(DT_BLOCK), 0, gb_stream(), nm, hflag, pos, hq);
+        GB_LAUNCH_CHECK();
+        *huge = hq;
+    }
+    gb_free(own_rp);
+    gb_free(own_ci);
+    gb_free(own_vx);
+    gb_free(own_perm);
+    return nh;
+}

@@ -87,6 +87,7 @@ struct GB_Matrix_opaque {
     int64_t *t_rowptr;
     int32_t *t_colidx;
     void *t_vals;
+    int64_t *t_perm;     // CSC position -> CSR position of the same entry
     // cached hub-chunk tables of the CSR (0) and CSC (1) orientation, built by
     // gb_view_hubs (gb_mxv.hip); dropped with the transpose
     int32_t *hub_tab[2];
@@ -262,6 +263,8 @@ void gb_view_nonempty(gb_csr_view &v, GB_Obj *A, int orient);
 void gb_view_long_rows(gb_csr_view &v, GB_Obj *A, int orient);
 // CSC of A (i.e. CSR of A^T), cached on the object when A is a matrix.
 void gb_get_csc(gb_csr_view &v, GB_Obj *A);
+// the cached CSC of a matrix and, per CSC entry, its CSR position (built on first use)
+const int64_t *gb_csc_perm(GB_Obj *A);
 // Values of a CSR view cast to type `code` (returns the view's own pointer if same type).
 const void *gb_view_vals_as(gb_csr_view &v, int code, gb_scratch &s);
 
@@ -302,9 +305,10 @@ void gb_extract_tuples(GB_Obj *A, GrB_Index *I, GrB_Index *J, void *X, int xcode
 void *gb_expand_iso(const void *one_value, size_t tsize, int64_t n);
 
 // transpose CSR -> CSR of the transpose (values optional)
+// tperm (optional): receives the CSC position -> CSR position map (caller frees)
 void gb_transpose_csr(int64_t nrows, int64_t ncols, int64_t nvals, const int64_t *rowptr,
                       const int32_t *colidx, const void *vals, size_t tsize, bool iso,
-                      int64_t **trowptr, int32_t **tcolidx, void **tvals);
+                      int64_t **trowptr, int32_t **tcolidx, void **tvals, int64_t **tperm = nullptr);
 
 // ------------------------------------------------------------------ ops
 struct gb_desc {
@@ -328,6 +332,7 @@ void gb_make_vmask(gb_vmask &m, GB_Obj *M, const gb_desc &d, int64_t n, bool all
 
 struct gb_mmask {
     bool present = false, comp = false;
+    GB_Obj *obj = nullptr;   // the mask matrix when rowptr/colidx are its own CSR (structural)
     gb_csr_view view;        // structure of the mask
     const int64_t *rowptr = nullptr;
     const int32_t *colidx = nullptr;
@@ -395,6 +400,7 @@ void gb_spgemm_hash(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, GrB_Semiri
 // scans / sorts (gb_prim.hip)
 void gb_exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n);  // out[n] = total
 void gb_exclusive_scan_u8(const uint8_t *in, int64_t *out, int64_t n);  // 0/1 flags, int64 prefixes
+void gb_exclusive_scan_i32(const int32_t *in, int64_t add_each, int64_t *out, int64_t n);  // of in[i] + add_each
 void gb_sort_pairs_u64(uint64_t *keys, int64_t *vals, int64_t n, int end_bit);
 void gb_sort_pairs_i32(int32_t *keys, int64_t *vals, int64_t n, int end_bit);
 int64_t gb_read_i64(const int64_t *dptr);

@@ -50,7 +50,7 @@ __global__ __launch_bounds__(MXM_BLOCK) void k_dot_masked(
     SR sr, int64_t nm, const int64_t *__restrict__ mrowof, const int32_t *__restrict__ mci,
     const int64_t *__restrict__ arp, const int32_t *__restrict__ aci, const X *__restrict__ avx, bool a_iso,
     const int64_t *__restrict__ brp, const int32_t *__restrict__ bci, const X *__restrict__ bvx, bool b_iso,
-    Z *__restrict__ tval, int64_t *__restrict__ tflag) {
+    Z *__restrict__ tval, uint8_t *__restrict__ tflag) {
     MXM_STRIDE(q, nm) {
         const int64_t i = mrowof[q];
         const int32_t j = mci[q];
@@ -109,11 +109,12 @@ __global__ __launch_bounds__(MXM_BLOCK) void k_dot_masked_group(
     SR sr, int64_t nm, const int64_t *__restrict__ mrowof, const int32_t *__restrict__ mci,
     const int64_t *__restrict__ arp, const int32_t *__restrict__ aci, const X *__restrict__ avx, bool a_iso,
     const int64_t *__restrict__ brp, const int32_t *__restrict__ bci, const X *__restrict__ bvx, bool b_iso,
-    Z *__restrict__ tval, int64_t *__restrict__ tflag) {
+    Z *__restrict__ tval, uint8_t *__restrict__ tflag, const int64_t *__restrict__ qlist) {
     const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     const int gl = (int)(tid & (G - 1));
     const int64_t ngroups = ((int64_t)gridDim.x * blockDim.x) / G;
-    for (int64_t q = tid / G; q < nm; q += ngroups) {
+    for (int64_t qq = tid / G; qq < nm; qq += ngroups) {
+        const int64_t q = qlist ? qlist[qq] : qq;  // a list of mask positions, or all of them
         const int64_t i = mrowof[q];
         const int32_t j = mci[q];
         const int64_t pa0 = arp[i], ea = arp[i + 1], pb0 = brp[j], eb = brp[j + 1];
@@ -214,7 +215,7 @@ __global__ void k_gather_rowptr(const int64_t *__restrict__ mrp, const int64_t *
 }
 
 template <class Z>
-__global__ void k_compact_dot(int64_t nm, const int64_t *__restrict__ flag, const int64_t *__restrict__ pos,
+__global__ void k_compact_dot(int64_t nm, const uint8_t *__restrict__ flag, const int64_t *__restrict__ pos,
                               const int32_t *__restrict__ mci, const Z *__restrict__ tval, int32_t *__restrict__ oci,
                               Z *__restrict__ ovx) {
     MXM_STRIDE(q, nm) {
@@ -316,6 +317,10 @@ __global__ void k_iso_value2(SR sr, const X *avals, const X *bvals, Z *out) {
     *out = sr.mult(a, b, 0, 0, 0);
 }
 
+// gb_dot.hip: masked dot, two-sided LDS method (exact monoids)
+int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &mask, const gb_sr_info &info,
+                         const void *av, const void *btv, void *tval, uint8_t *tflag, int64_t **huge);
+
 void gb_spgemm(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, gb_csr_view *BT, gb_mmask &mask,
                GrB_Semiring sr) {
     gb_sr_info info = gb_sr_describe(sr);
@@ -337,25 +342,48 @@ void gb_spgemm(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, gb_csr_view *BT
     if (use_dot) {
         const void *btv = info.reads_values ? gb_view_vals_as(*BT, info.xcode, s) : nullptr;
         const int64_t nm = mask.nvals;
-        int64_t *mrowof = s.get<int64_t>(nm);
-        if (nm)
-            hipLaunchKernelGGL(k_rowof, dim3(mxm_grid(std::min<int64_t>(nrows * 64, 1LL << 22))), dim3(MXM_BLOCK), 0,
-                               gb_stream(), mask.rowptr, (int64_t)0, nrows, (int64_t)0, mrowof);
-        int64_t *flag = s.get<int64_t>(nm);
+        uint8_t *flag = s.get<uint8_t>(nm);
         int64_t *pos = s.get<int64_t>(nm + 1);
         void *tval = s.get<char>(nm * zs);
+        int64_t *mrowof = nullptr;
+        auto rowof = [&]() {
+            mrowof = s.get<int64_t>(nm);
+            hipLaunchKernelGGL(k_rowof, dim3(mxm_grid(std::min<int64_t>(nrows * 64, 1LL << 22))), dim3(MXM_BLOCK), 0,
+                               gb_stream(), mask.rowptr, (int64_t)0, nrows, (int64_t)0, mrowof);
+        };
         gb_dispatch_sr(info, [&](auto srf, auto x, auto z) {
             using SRT = decltype(srf);
             using X = decltype(x);
             using Z = decltype(z);
             int64_t gsel = gb_knob("dot_group");  // 0 auto (a wave per entry), 1 thread per entry, else lanes
             if (gsel == 0) gsel = 64;
-            if (nm && gsel > 1 && exact_monoid(info.mon, info.zcode)) {
+            const bool exact = exact_monoid(info.mon, info.zcode);
+            // the two-sided LDS method (gb_dot.hip) folds into monoid identities: not for
+            // float MIN/MAX, whose NaN-ignoring fold of only-NaN terms differs from the identity's
+            const bool float_minmax = (info.zcode == GBAMD_T_FP32 || info.zcode == GBAMD_T_FP64) &&
+                                      (info.mon == GBAMD_MON_MIN || info.mon == GBAMD_MON_MAX);
+            const bool any_pair = info.mon == GBAMD_MON_ANY && info.mul == GBAMD_OP_PAIR;
+            const bool two_sided = nm && (exact || any_pair) && !float_minmax && gb_knob("dot_method") != 1;
+            if (nm) gb_memset(flag, 0, nm);
+            if (two_sided) {
+                int64_t *hq = nullptr;
+                const int64_t nh = gb_dot_two_sided(A, *BT, mask, info, av, btv, tval, flag, &hq);
+                if (nh) {
+                    rowof();
+                    const unsigned g = mxm_grid(std::min<int64_t>(nh * 64, 1LL << 24));
+                    hipLaunchKernelGGL((k_dot_masked_group<SRT, X, Z, 64>), dim3(g), dim3(MXM_BLOCK), 0, gb_stream(),
+                                       srf, nh, mrowof, mask.colidx, A.rowptr, A.colidx, (const X *)av, A.iso,
+                                       BT->rowptr, BT->colidx, (const X *)btv, BT->iso, (Z *)tval, flag, hq);
+                    GB_LAUNCH_CHECK();
+                    gb_free(hq);
+                }
+            } else if (nm && gsel > 1 && exact) {
+                rowof();
                 const unsigned g = mxm_grid(std::min<int64_t>(nm * gsel, 1LL << 24));
 #define GB_DOT_GROUP(GG)                                                                                 \
     hipLaunchKernelGGL((k_dot_masked_group<SRT, X, Z, GG>), dim3(g), dim3(MXM_BLOCK), 0, gb_stream(), srf, nm, \
                        mrowof, mask.colidx, A.rowptr, A.colidx, (const X *)av, A.iso, BT->rowptr, BT->colidx, \
-                       (const X *)btv, BT->iso, (Z *)tval, flag)
+                       (const X *)btv, BT->iso, (Z *)tval, flag, (const int64_t *)nullptr)
                 if (gsel <= 4) GB_DOT_GROUP(4);
                 else if (gsel <= 8) GB_DOT_GROUP(8);
                 else if (gsel <= 16) GB_DOT_GROUP(16);
@@ -363,12 +391,13 @@ void gb_spgemm(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, gb_csr_view *BT
                 else GB_DOT_GROUP(64);
 #undef GB_DOT_GROUP
             } else if (nm) {
+                rowof();
                 hipLaunchKernelGGL((k_dot_masked<SRT, X, Z>), dim3(mxm_grid(nm)), dim3(MXM_BLOCK), 0, gb_stream(),
                                    srf, nm, mrowof, mask.colidx, A.rowptr, A.colidx, (const X *)av, A.iso,
                                    BT->rowptr, BT->colidx, (const X *)btv, BT->iso, (Z *)tval, flag);
             }
             GB_LAUNCH_CHECK();
-            gb_exclusive_scan_i64(flag, pos, nm);
+            gb_exclusive_scan_u8(flag, pos, nm);
             int64_t nz = gb_read_i64(pos + nm);
             T.rowptr = gb_malloc_n<int64_t>(nrows + 1);
             hipLaunchKernelGGL(k_gather_rowptr, dim3(mxm_grid(nrows + 1)), dim3(MXM_BLOCK), 0, gb_stream(),

@@ -238,12 +238,6 @@ struct gb_wlist {
     int8_t hit[WL_MAX];   // a k present in u was found this round
 };
 
-__device__ __forceinline__ void gb_wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 // this round takes min(rem[i], cap) edges of segment i; hit[i] = 0; pref = inclusive
 // prefix of the taken lengths; returns the total
 __device__ __forceinline__ int gb_wlist_round(gb_wlist &L, int n, int cap, int lane) {

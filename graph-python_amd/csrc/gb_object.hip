@@ -109,7 +109,9 @@ void gb_drop_transpose(GB_Obj *A) {
         gb_free(A->t_rowptr);
         gb_free(A->t_colidx);
         gb_free(A->t_vals);
+        gb_free(A->t_perm);
     }
+    A->t_perm = nullptr;
     A->t_rowptr = nullptr;
     A->t_colidx = nullptr;
     A->t_vals = nullptr;
@@ -269,7 +271,7 @@ void gb_get_csc(gb_csr_view &v, GB_Obj *A) {
     if (A->kind == GB_KIND_MATRIX) {
         if (!A->t_valid) {
             gb_transpose_csr(A->nrows, A->ncols, A->nvals, A->rowptr, A->colidx, A->vals,
-                             A->type->size, A->iso, &A->t_rowptr, &A->t_colidx, &A->t_vals);
+                             A->type->size, A->iso, &A->t_rowptr, &A->t_colidx, &A->t_vals, &A->t_perm);
             A->t_valid = true;
         }
         v.nrows = A->ncols;
@@ -298,6 +300,13 @@ void gb_get_csc(gb_csr_view &v, GB_Obj *A) {
     v.colidx = tci;
     v.vals = tvx;
     v.iso = c.iso;
+}
+
+const int64_t *gb_csc_perm(GB_Obj *A) {
+    GB_REQUIRE(A->kind == GB_KIND_MATRIX, GrB_INVALID_VALUE, "CSC position map of a non-matrix");
+    gb_csr_view v;
+    gb_get_csc(v, A);
+    return A->t_perm;
 }
 
 const void *gb_view_vals_as(gb_csr_view &v, int code, gb_scratch &s) {

@@ -55,6 +55,16 @@ void gb_exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n) {
     scan_chunked(in, out, n);
 }
 
+struct gb_i32_plus {
+    int64_t add;
+    __host__ __device__ int64_t operator()(int32_t x) const { return (int64_t)x + add; }
+};
+
+void gb_exclusive_scan_i32(const int32_t *in, int64_t add_each, int64_t *out, int64_t n) {
+    scan_chunked(hipcub::TransformInputIterator<int64_t, gb_i32_plus, const int32_t *>(in, gb_i32_plus{add_each}), out,
+                 n);
+}
+
 void gb_exclusive_scan_u8(const uint8_t *in, int64_t *out, int64_t n) {
     // as gb_exclusive_scan_i64 over 0/1 byte flags, summed in int64
     scan_chunked(hipcub::TransformInputIterator<int64_t, gb_u8_to_i64, const uint8_t *>(in, gb_u8_to_i64()), out, n);
@@ -387,7 +397,7 @@ __global__ void k_transpose_fill(const int64_t *__restrict__ perm, const int64_t
 
 void gb_transpose_csr(int64_t nrows, int64_t ncols, int64_t nvals, const int64_t *rowptr,
                       const int32_t *colidx, const void *vals, size_t tsize, bool iso,
-                      int64_t **trowptr, int32_t **tcolidx, void **tvals) {
+                      int64_t **trowptr, int32_t **tcolidx, void **tvals, int64_t **tperm) {
     int64_t *trp = gb_malloc_n<int64_t>(ncols + 1);
     int32_t *tci = gb_malloc_n<int32_t>(nvals);
     void *tvx = vals ? (iso ? gb_malloc(tsize) : gb_malloc(nvals * tsize)) : nullptr;
@@ -435,8 +445,14 @@ void gb_transpose_csr(int64_t nrows, int64_t ncols, int64_t nvals, const int64_t
         }
         GB_LAUNCH_CHECK();
         gb_free(keys);
+        if (tperm) {
+            *tperm = perm;
+            perm = nullptr;
+        }
         gb_free(perm);
         gb_free(rowof);
+    } else if (tperm) {
+        *tperm = gb_malloc_n<int64_t>(1);
     }
     *trowptr = trp;
     *tcolidx = tci;

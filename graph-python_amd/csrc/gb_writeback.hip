@@ -121,6 +121,7 @@ void gb_make_mmask(gb_mmask &m, GB_Obj *M, const gb_desc &d, int64_t nrows, int6
         m.rowptr = m.view.rowptr;
         m.colidx = m.view.colidx;
         m.nvals = m.view.nvals;
+        if (M->kind == GB_KIND_MATRIX) m.obj = M;
         return;
     }
     int64_t *cnt = m.own.get<int64_t>(nrows + 1);

@@ -787,3 +787,84 @@ def test_deferred_assign_failure_is_recorded_on_its_vector(gb):
     with pytest.raises(ex.InvalidObject):
         v.nvals
     assert q.nvals == 3 and other.nvals == 2
+
+
+def _skewed_both(rng, n, dtype):
+    """long rows AND long columns (the union of a row-skewed matrix and the transpose of
+    another), so both phases of the two-sided masked dot get task-sized groups."""
+    R, T = _skewed_csr(rng, n, dtype), _skewed_csr(rng, n, dtype)
+    r1, c1, v1 = R.to_coo()
+    r2, c2, v2 = T.to_coo()
+    r, c, v = np.concatenate([r1, c2]), np.concatenate([c1, r2]), np.concatenate([v1, v2])
+    key, idx = np.unique(r * n + c, return_index=True)
+    return O.Csr.from_coo(key // n, key % n, v[idx], nrows=n, ncols=n, dtype=dtype)
+
+
+TWO_SIDED = [
+    ("min_plus", "MIN", "PLUS", "INT64"),
+    ("plus_times", "PLUS", "TIMES", "INT64"),
+    ("max_plus", "MAX", "PLUS", "INT32"),
+    ("plus_pair", "PLUS", "PAIR", "INT64"),
+    ("any_pair", "ANY", "PAIR", "INT64"),
+    ("any_pair", "ANY", "PAIR", "BOOL"),
+    ("lor_land", "LOR", "LAND", "BOOL"),
+    ("min_first", "MIN", "FIRST", "UINT64"),
+    ("max_second", "MAX", "SECOND", "INT16"),
+    ("min_secondi", "MIN", "SECONDI", "INT64"),
+    ("plus_min", "PLUS", "MIN", "UINT8"),
+    ("times_plus", "TIMES", "PLUS", "INT32"),
+]
+
+
+@pytest.mark.parametrize("name,mon,mul,dt", TWO_SIDED)
+@pytest.mark.parametrize("knobs", [(0, 0), (128, 256)])  # (dot_cap, dot_win): defaults / every path forced
+@pytest.mark.parametrize("form", ["AA_struct", "AAT_struct", "ATA_value", "AB_rect"])
+def test_masked_spgemm_two_sided_vs_oracle(gb, name, mon, mul, dt, knobs, form):
+    """The two-sided LDS masked dot (gb_dot.hip): entries grouped by the side owning the
+    longer list -- mask rows (CSR) or mask columns (the mask's CSC + position map, cached
+    on a structural mask matrix, built per call for a value mask) -- in the small-group,
+    task and per-entry kernels; shrunken cap/window knobs send hub lists to the per-entry
+    kernel and cut groups into many tasks.  Bit-exact vs the oracle."""
+    rng = np.random.default_rng(hash((name, dt, form, knobs)) % 2**32)
+    n = 1500
+    Ao = _skewed_both(rng, n, dt)
+    sr = getattr(gb.semiring, name)[dt]
+    Ag = _to_gb(gb, Ao)
+    cap, win = knobs
+    gb.set_knob("dot_cap", cap)
+    gb.set_knob("dot_win", win)
+    try:
+        if form == "AA_struct":
+            Cg = Ag.mxm(Ag, sr).new(mask=Ag.S)
+            ref = O.mxm(O.Csr.empty(n, n, dt), Ao, Ao, (mon, mul, dt), mask=Ao, mask_struct=True)
+        elif form == "AAT_struct":
+            Mo = _skewed_both(rng, n, "BOOL")
+            Mg = _to_gb(gb, Mo)
+            Cg = Ag.mxm(Ag.T, sr).new(mask=Mg.S)
+            ref = O.mxm(O.Csr.empty(n, n, dt), Ao, Ao, (mon, mul, dt), mask=Mo, mask_struct=True, tran1=True)
+        elif form == "ATA_value":
+            Mo = _skewed_both(rng, n, "BOOL")
+            Mg = _to_gb(gb, Mo)
+            Cg = Ag.T.mxm(Ag, sr).new(mask=Mg.V)
+            ref = O.mxm(O.Csr.empty(n, n, dt), Ao, Ao, (mon, mul, dt), mask=Mo, tran0=True)
+        else:
+            k, m = 900, 1100
+            Bo = _skewed_both(rng, 1200, dt)
+            r, c, v = Bo.to_coo()
+            keep = (r < k) & (c < m)
+            Bo = O.Csr.from_coo(r[keep], c[keep], v[keep], nrows=k, ncols=m, dtype=dt)
+            r, c, v = Ao.to_coo()
+            keep = c < k
+            A2 = O.Csr.from_coo(r[keep], c[keep], v[keep], nrows=n, ncols=k, dtype=dt)
+            Mo = _rand_csr(rng, n, m, 0.05, "BOOL")
+            Cg = _to_gb(gb, A2).mxm(_to_gb(gb, Bo), sr).new(mask=_to_gb(gb, Mo).S)
+            ref = O.mxm(O.Csr.empty(n, m, dt), A2, Bo, (mon, mul, dt), mask=Mo, mask_struct=True)
+    finally:
+        gb.set_knob("dot_cap", 0)
+        gb.set_knob("dot_win", 0)
+    if mon == "ANY":
+        r, c, _ = Cg.to_coo()
+        er, ec, _ = ref.to_coo()
+        assert np.array_equal(r.astype(np.int64), er) and np.array_equal(c.astype(np.int64), ec)
+    else:
+        _check_mat(Cg, ref)

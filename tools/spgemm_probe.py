@@ -49,7 +49,12 @@ def run():
 
 
 for g in sys.argv[3:] or ["0"]:
-    gb.set_knob("dot_group", int(g))
+    # "k=v" sets a knob for this measurement, a bare number sets dot_group
+    if "=" in g:
+        kk, vv = g.split("=")
+        gb.set_knob(kk, int(vv))
+    else:
+        gb.set_knob("dot_group", int(g))
     run()
     torch.cuda.synchronize()
     ts = []
@@ -59,5 +64,5 @@ for g in sys.argv[3:] or ["0"]:
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
     t = min(ts)
-    print(f"s{scale} dot_group {g}: nnz(A) {nnz} nnz(C) {nc} work {work:.3e} time {t*1e3:.2f} ms "
+    print(f"s{scale} {g}: nnz(A) {nnz} nnz(C) {nc} work {work:.3e} time {t*1e3:.2f} ms "
           f"GTEPS {work / t / 1e9:.2f}", flush=True)
