@@ -83,7 +83,7 @@ __global__ __launch_bounds__(DT_BLOCK) void k_dt_classify(dt_side s, int cap, ui
         for (int64_t p = s.grp_rp[g] + lane; p < s.grp_rp[g + 1]; p += 64) {
             const int32_t o = s.grp_oi[p];
             const int64_t b = s.yrp[o + 1] - s.yrp[o];
-            if (!dt_side_of<SWAP>(a, b)) continue;
+            if (b == 0 || !dt_side_of<SWAP>(a, b)) continue;  // an empty Y list matches nothing
             if (a <= cap) tflag[p] = 1;
             else hflag[s.perm ? s.perm[p] : p] = 1;
         }
@@ -282,21 +282,35 @@ __global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, dt_side s, const 
 // come precomputed in task order (k_dt_compact).
 //  1. X(g,:)'s keys go to LDS as they are (sorted) plus a hashed membership filter
 //     (2^18 bits, <= 6.25 % set): one LDS read rejects most Y keys.
-//  2. Entries are cut into units of <= DT_PIECE elements of their Y list; waves
-//     take units from an LDS counter.  In a unit the wave streams Y's keys 64 lanes
-//     wide (coalesced), DT_U loads in flight per lane, filters them, packs the
-//     keys that pass (~hits + 6 %) densely into a per-wave LDS stage and binary-
-//     searches those in X's keys with every lane busy; hits load both values and
-//     fold in registers, one wave fold per unit.  A one-unit entry is written
-//     straight to T; a longer entry's units meet in an LDS slot (atomic fold of an
-//     exact monoid) written at the end of the task.
+//  2. The entries' Y lists form one flat element space (prefix e_pre), cut into
+//     units of DT_PIECE elements that waves take from an LDS counter -- a unit may
+//     hold many short entries, so every wave keeps DT_U * 64 loads in flight
+//     whatever the entries' lengths.  A lane finds its element's entry from a
+//     bitmap of entry starts over the flat space (one 64-bit word per 64 elements,
+//     a popcount), loads the Y key (coalesced), filters it, and packs the keys that
+//     pass (~hits + 6 %) densely into a per-wave LDS stage; the stage is binary-
+//     searched in X's keys with every lane busy.  Hits fold in registers per lane
+//     (a lane's staged elements come in entry order) and meet per entry in LDS
+//     slots (atomic fold of an exact monoid, one per lane run -- one per wave when
+//     the wave's hits share an entry), written to T at the end of the task.
 constexpr int DT_TB = 1024;      // task workgroup: 16 waves, one workgroup per CU
-constexpr int DT_U = 4;          // Y keys in flight per lane
-constexpr int DT_PIECE = 1024;   // elements per unit
-constexpr int DT_MAXU = DT_MAXE + DT_WIN / DT_PIECE + DT_CAP / DT_PIECE + 2;  // units per task bound
+constexpr int DT_U = 8;          // 64-element windows per step (loads in flight per lane)
+constexpr int DT_PIECE = 1024;   // elements per unit (a multiple of 64 * DT_U)
+constexpr int DT_SMAX = DT_WIN + DT_CAP;  // flat elements per task bound
 constexpr int DT_FLOG = 18;      // filter bits (log2)
 
 __device__ __forceinline__ uint32_t dt_hash(int32_t k) { return ((uint32_t)k * 0x9E3779B1u) >> (32 - DT_FLOG); }
+
+template <class SR, class Z>
+__device__ __forceinline__ void dt_slot_fold(const SR &sr, bool any_store, unsigned long long *slot, Z z) {
+    if (any_store) {
+        unsigned long long v = 0;
+        __builtin_memcpy(&v, &z, sizeof(Z));
+        *slot = v;
+    } else {
+        dt_lds_fold(sr, slot, z);
+    }
+}
 
 template <class SR, class X, class Z, bool SWAP>
 __global__ __launch_bounds__(DT_TB) void k_dot_task(
@@ -306,14 +320,12 @@ __global__ __launch_bounds__(DT_TB) void k_dot_task(
     const int64_t *__restrict__ eQ, Z *__restrict__ tval, uint8_t *__restrict__ tflag, int dbg) {
     __shared__ int32_t keys[DT_CAP];
     __shared__ uint32_t filt[1 << (DT_FLOG - 5)];
-    __shared__ int32_t stage_k[DT_TB / 64][64 * DT_U];
-    __shared__ int32_t stage_f[DT_TB / 64][64 * DT_U];
+    __shared__ uint64_t estart[DT_SMAX / 64 + 1];     // bit f: an entry starts at flat element f
+    __shared__ int32_t stage[DT_TB / 64][64 * DT_U];  // staged flat element | entry << 17
     __shared__ int64_t e_ys[DT_MAXE];
     __shared__ int64_t e_q[DT_MAXE];
     __shared__ int32_t e_o[DT_MAXE];
-    __shared__ int32_t e_b[DT_MAXE];
-    __shared__ int32_t e_upre[DT_MAXE + 1];
-    __shared__ int16_t u2e[DT_MAXU];
+    __shared__ int32_t e_pre[DT_MAXE + 1];
     __shared__ unsigned long long e_acc[DT_MAXE];
     __shared__ int e_fnd[DT_MAXE];
     __shared__ int w_sum[DT_TB / 64];
@@ -325,29 +337,27 @@ __global__ __launch_bounds__(DT_TB) void k_dot_task(
     const bool ANY = std::is_same<SR, gb_sr_any_pair<Z>>::value || mon == GBAMD_MON_ANY;
     const Z ident = ANY ? Z() : gb_monoid_identity<Z>(mon);
     const unsigned long long ltmask = (1ULL << lane) - 1;
-    int32_t *stk = stage_k[wid];
-    int32_t *stf = stage_f[wid];
+    int32_t *stg = stage[wid];
     for (int64_t t = blockIdx.x; t < ntask; t += gridDim.x) {
         const int64_t e0 = tstart[t];
-        const int ne = (int)(tstart[t + 1] - e0);
+        const int ne = __builtin_amdgcn_readfirstlane((int)(tstart[t + 1] - e0));
         const int64_t g = eG[e0];
         const int64_t xs = s.xrp[g];
-        const int a = (int)(s.xrp[g + 1] - xs);
+        const int a = __builtin_amdgcn_readfirstlane((int)(s.xrp[g + 1] - xs));
         for (int i = tid; i < (1 << (DT_FLOG - 5)); i += DT_TB) filt[i] = 0;
-        int nu = 0;
+        for (int i = tid; i < DT_SMAX / 64 + 1; i += DT_TB) estart[i] = 0;
+        int b = 0;
         if (tid < ne) {
-            const int b = eB[e0 + tid];
+            b = eB[e0 + tid];
             e_ys[tid] = eYS[e0 + tid];
             e_o[tid] = eO[e0 + tid];
-            e_b[tid] = b;
             e_q[tid] = eQ[e0 + tid];
             unsigned long long iv = 0;
             __builtin_memcpy(&iv, &ident, sizeof(Z));
             e_acc[tid] = iv;
             e_fnd[tid] = 0;
-            nu = (b + DT_PIECE - 1) / DT_PIECE;
         }
-        int inc = nu;
+        int inc = b;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
             const int y = __shfl_up(inc, off, 64);
@@ -355,68 +365,85 @@ __global__ __launch_bounds__(DT_TB) void k_dot_task(
         }
         if (lane == 63) w_sum[wid] = inc;
         if (tid == 0) next_unit = 0;
-        __syncthreads();  // filter cleared, unit counts visible
+        __syncthreads();  // filter and start bits cleared, wave sums visible
         for (int i = tid; i < a; i += DT_TB) {
             const int32_t k = s.xci[xs + i];
             keys[i] = k;
             const uint32_t h = dt_hash(k);
             atomicOr(&filt[h >> 5], 1u << (h & 31));
         }
-        int base = 0, NU = 0;
+        int base = 0, S = 0;
         for (int w = 0; w < DT_TB / 64; w++) {
             if (w < wid) base += w_sum[w];
-            NU += w_sum[w];
+            S += w_sum[w];
         }
+        S = __builtin_amdgcn_readfirstlane(S);
         if (tid < ne) {
-            e_upre[tid] = base + inc - nu;
-            for (int u = base + inc - nu; u < base + inc; u++) u2e[u] = (int16_t)tid;
+            const int f = base + inc - b;
+            e_pre[tid] = f;
+            if (b > 0) atomicOr((unsigned long long *)&estart[f >> 6], 1ULL << (f & 63));
         }
-        if (tid == 0) e_upre[ne] = NU;
+        if (tid == 0) e_pre[ne] = S;
         __syncthreads();
-        int ksteps = 0;
+        int ksteps = 0, esteps = 0;
         while ((1 << ksteps) < a) ksteps++;
-        // units: wave-uniform bookkeeping kept in scalar registers (readlane), so the
-        // loop exit and the trip counts are scalar branches
+        while ((1 << esteps) < ne) esteps++;
+        const int NU = (S + DT_PIECE - 1) / DT_PIECE;
+        // units (wave-uniform bookkeeping in scalar registers; no `continue` in the
+        // loop: its body holds cross-lane operations)
         int unit = 0;
         if (lane == 0) unit = atomicAdd(&next_unit, 1);
         unit = __builtin_amdgcn_readlane(unit, 0);
         while (unit < NU) {
-            const int e = __builtin_amdgcn_readfirstlane((int)u2e[unit]);
-            const int64_t ys_v = e_ys[e];
-            const int64_t ys = ((int64_t)__builtin_amdgcn_readfirstlane((int)(ys_v >> 32)) << 32) |
-                               (uint32_t)__builtin_amdgcn_readfirstlane((int)ys_v);
-            const int b = __builtin_amdgcn_readfirstlane(e_b[e]);
-            const int o = __builtin_amdgcn_readfirstlane(e_o[e]);
-            const int u0 = (unit - __builtin_amdgcn_readfirstlane(e_upre[e])) * DT_PIECE;
-            const int u1 = min(u0 + DT_PIECE, b);
+            const int fu0 = unit * DT_PIECE, fu1 = min(S, fu0 + DT_PIECE);
+            // entry holding fu0 (last e with e_pre[e] <= fu0; empty entries resolve
+            // to the last of equal starts, which the bitmap walk also does)
+            int ew = 0;
+            for (int st = esteps - 1; st >= 0; st--) {
+                const int c = ew + (1 << st);
+                if (c < ne && e_pre[c] <= fu0) ew = c;
+            }
+            ew = __builtin_amdgcn_readfirstlane(ew);
+            int cur_e = -1;
             bool found = false;
             Z acc = Z();
-            for (int f0 = u0; f0 < ((dbg & 8) ? u0 : u1); f0 += 64 * DT_U) {
+            for (int f0 = fu0; f0 < ((dbg & 8) ? fu0 : fu1); f0 += 64 * DT_U) {
+                int cnt = 0;
                 int32_t k[DT_U];
+                int ee[DT_U];
+                int64_t py[DT_U];
+#pragma unroll
+                for (int u = 0; u < DT_U; u++) {
+                    // entries starting in this 64-element window, then the lane's entry
+                    const int fw = f0 + u * 64;
+                    const uint64_t sb = estart[fw >> 6];
+                    const int f = fw + lane;
+                    // a start at the window's first element is counted by the popcount
+                    // (ew holds the entry of the element before it)
+                    int e_l = ew + __popcll(sb & ((ltmask << 1) | 1ULL));
+                    if (fw == fu0 && (sb & 1ULL)) e_l -= 1;  // unit start: ew already is that entry
+                    ee[u] = e_l;
+                    const int eL = e_l < ne ? e_l : ne - 1;
+                    py[u] = e_ys[eL] + (f - e_pre[eL]);
+                    ew = __builtin_amdgcn_readfirstlane(__shfl(e_l, 63, 64));
+                    k[u] = f < fu1 ? ((dbg & 4) ? f : s.yci[py[u]]) : -1;
+                }
 #pragma unroll
                 for (int u = 0; u < DT_U; u++) {
                     const int f = f0 + u * 64 + lane;
-                    k[u] = f < u1 ? ((dbg & 4) ? f : s.yci[ys + f]) : -1;
-                }
-                // filter, then pack the keys that pass into the wave's stage
-                int cnt = 0;
-#pragma unroll
-                for (int u = 0; u < DT_U; u++) {
                     const uint32_t h = dt_hash(k[u]);
-                    const bool c = !(dbg & 2) && f0 + u * 64 + lane < u1 && ((filt[h >> 5] >> (h & 31)) & 1u);
+                    const bool c = !(dbg & 2) && f < fu1 && ((filt[h >> 5] >> (h & 31)) & 1u);
                     const unsigned long long m = __ballot(c);
-                    if (c) {
-                        const int idx = cnt + __popcll(m & ltmask);
-                        stk[idx] = k[u];
-                        stf[idx] = f0 + u * 64 + lane;
-                    }
+                    if (c) stg[cnt + __popcll(m & ltmask)] = f | (ee[u] << 17);
                     cnt += __popcll(m);
                 }
                 gb_wave_sync();
                 for (int r = 0; r < cnt; r += 64) {
                     const bool act = r + lane < cnt;
-                    const int32_t kk = act ? stk[r + lane] : -1;
-                    const int ff = act ? stf[r + lane] : 0;
+                    const int w = act ? stg[r + lane] : 0;
+                    const int f = w & 0x1ffff, e = w >> 17;
+                    const int64_t p = act ? e_ys[e] + (f - e_pre[e]) : 0;
+                    const int32_t kk = act ? s.yci[p] : -1;
                     int l = 0;  // number of X keys < kk
                     for (int st = ksteps - 1; st >= 0; st--) {
                         const int c = l + (1 << st);
@@ -426,31 +453,36 @@ __global__ __launch_bounds__(DT_TB) void k_dot_task(
                         X xv = X(), yv = X();
                         if (rv) {
                             xv = xvx[x_iso ? 0 : xs + l];
-                            yv = yvx[y_iso ? 0 : ys + ff];
+                            yv = yvx[y_iso ? 0 : p];
                         }
-                        const Z z = dt_mult<SR, X, Z, SWAP>(sr, xv, yv, g, kk, o);
+                        const Z z = dt_mult<SR, X, Z, SWAP>(sr, xv, yv, g, kk, e_o[e]);
+                        if (e != cur_e) {  // a lane's staged elements come in entry order
+                            if (found) {
+                                dt_slot_fold(sr, ANY, &e_acc[cur_e], acc);
+                                e_fnd[cur_e] = 1;
+                            }
+                            cur_e = e;
+                            found = false;
+                        }
                         acc = found ? sr.add(acc, z) : z;
                         found = true;
                     }
                 }
                 gb_wave_sync();  // the stage is rewritten by the next step
             }
-            if (__ballot(found)) {
-                dt_wave_fold(sr, found, acc);
-                if (lane == 0) {
-                    if (b <= DT_PIECE) {
-                        tval[e_q[e]] = acc;
-                        tflag[e_q[e]] = 1;
-                    } else {
-                        if (ANY) {
-                            unsigned long long v = 0;
-                            __builtin_memcpy(&v, &acc, sizeof(Z));
-                            e_acc[e] = v;
-                        } else {
-                            dt_lds_fold(sr, &e_acc[e], acc);
-                        }
-                        e_fnd[e] = 1;
+            // end of the unit: one fold per wave when every lane's run is one entry
+            const unsigned long long fb = __ballot(found);
+            if (fb) {
+                const int e_first = __builtin_amdgcn_readlane(cur_e, __builtin_ctzll(fb));
+                if (!__ballot(found && cur_e != e_first)) {
+                    dt_wave_fold(sr, found, acc);
+                    if (lane == 0) {
+                        dt_slot_fold(sr, ANY, &e_acc[e_first], acc);
+                        e_fnd[e_first] = 1;
                     }
+                } else if (found) {
+                    dt_slot_fold(sr, ANY, &e_acc[cur_e], acc);
+                    e_fnd[cur_e] = 1;
                 }
             }
             int nxt = 0;
@@ -458,7 +490,7 @@ __global__ __launch_bounds__(DT_TB) void k_dot_task(
             unit = __builtin_amdgcn_readlane(nxt, 0);
         }
         __syncthreads();
-        if (tid < ne && e_b[tid] > DT_PIECE && e_fnd[tid]) {
+        if (tid < ne && e_fnd[tid]) {
             Z v;
             const unsigned long long raw = e_acc[tid];
             __builtin_memcpy(&v, &raw, sizeof(Z));
