@@ -204,8 +204,10 @@ __global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, dt_side s, const 
         int32_t xk[KPL];
 #pragma unroll
         for (int j = 0; j < KPL; j++) xk[j] = lane * KPL + j < a ? s.xci[xs + lane * KPL + j] : 0x7fffffff;
-        X xv = X();
-        if (KPL == 1 && rv && lane < a) xv = xvx[x_iso ? 0 : xs + lane];
+        // X's values held beside the keys (read by a shuffle on a hit, no dependent load)
+        X xv[KPL];
+#pragma unroll
+        for (int j = 0; j < KPL; j++) xv[j] = (rv && lane * KPL + j < a) ? xvx[x_iso ? 0 : xs + lane * KPL + j] : X();
         for (int64_t pb = p0; pb < p1; pb += 64) {
             const int nb = __builtin_amdgcn_readfirstlane((int)std::min<int64_t>(64, p1 - pb));
             int32_t o_l = 0;
@@ -236,7 +238,7 @@ __global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, dt_side s, const 
                                 if (__shfl(xk[0], lo + st - 1, 64) < yk) lo += st;
                             // every lane takes part in the shuffle (a lane outside |Y| still serves its key)
                             const int32_t xl = __shfl(xk[0], lo, 64);
-                            xm = gb_shfl(xv, lo);
+                            xm = gb_shfl(xv[0], lo);
                             if (act && xl == yk) pos = lo;
                         } else {
                             int L = 0;  // last lane whose first key <= yk
@@ -249,9 +251,12 @@ __global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, dt_side s, const 
 #pragma unroll
                             for (int j = 0; j < KPL; j++) {
                                 const int32_t v = __shfl(xk[j], L, 64);
-                                if (act && v == yk) pos = L * KPL + j;
+                                const X vx = gb_shfl(xv[j], L);
+                                if (act && v == yk) {
+                                    pos = L * KPL + j;
+                                    xm = vx;
+                                }
                             }
-                            if (rv && pos >= 0) xm = xvx[x_iso ? 0 : xs + pos];
                         }
                         if (pos >= 0) {
                             X yv = X();
