@@ -657,6 +657,7 @@ struct gb_iso_args {
     int64_t spare_words;
     // pull shape: lane-per-row steps of 4 edges, then the first per-row cap of the list rounds
     int p1_steps, cap0;
+    int dbg;                        // diagnostics (knob iso_dbg): 1 no mailbox, 2 no hint sum, 4 no work
     const uint64_t *rows_nonempty;  // pull rows with entries (nullptr: all)
     // fused deferred assign (gb_asg): w<q>(:) = x with q = u (asg.bits nullptr: none)
     gb_asg_dev asg;
@@ -676,6 +677,7 @@ struct gb_iso_args {
 // combined in chunk order by k_spmv_fold.
 #define SPMV_LONG 128
 #define SPMV_CH 1024
+#define SPMV_WU 8  // entries per lane per step of the words kernel (gathers in flight)
 
 template <class SR, class X, class Z, bool FLIP>
 __device__ __forceinline__ void gb_spmv_product(SR &sr, bool rv, const X *__restrict__ avals, bool a_iso, X a0,
@@ -950,12 +952,13 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
         }
         const int excl = incl - len;
         const int total = __shfl(incl, 63, 64);
-        for (int e0 = 0; e0 < total; e0 += 256) {
-            int k[4], own[4];
-            int64_t pos[4];
-            bool ok[4];
+        for (int e0 = 0; e0 < total; e0 += 64 * SPMV_WU) {
+            // all SPMV_WU gathers of the step are issued before the first fold waits on one
+            int k[SPMV_WU], own[SPMV_WU];
+            int64_t pos[SPMV_WU];
+            bool ok[SPMV_WU];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < SPMV_WU; u++) {
                 const int e = e0 + lane + 64 * u;
                 int lo = 0;
 #pragma unroll
@@ -966,13 +969,20 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
                 ok[u] = e < total;
                 k[u] = ok[u] ? colidx[pos[u]] : 0;
             }
+            bool fu[SPMV_WU];
+            Z zu[SPMV_WU];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                bool f = ok[u] && (ufull || gb_bit(ubits, k[u]));
-                Z z = Z();
-                if (f)
+            for (int u = 0; u < SPMV_WU; u++) {
+                fu[u] = ok[u] && (ufull || gb_bit(ubits, k[u]));
+                zu[u] = Z();
+                if (fu[u])
                     gb_spmv_product<SR, X, Z, FLIP>(sr, rv, avals, a_iso, a0, uvals, u_iso, u0, pos[u], k[u],
-                                                    (w << 6) + own[u], z);
+                                                    (w << 6) + own[u], zu[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < SPMV_WU; u++) {
+                bool f = fu[u];
+                Z z = zu[u];
                 // segmented inclusive scan over lanes of the same row
                 const int row = ok[u] ? own[u] : 64 + lane;  // idle lanes: own segment
                 for (int off = 1; off < 64; off <<= 1) {
@@ -1055,8 +1065,10 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
     // fused assign: q's value mask is empty when q is iso with a false value
     const uint64_t *qbits = nullptr;
     if (a.asg.bits && (!a.asg_qiso || gb_dyn_nonzero(a.asg_qiso, a.asg_qiso_code))) qbits = ubits;
-    long long mfn = 0, cnt, adelta = 0;
-    if (push)
+    long long mfn = 0, cnt = 0, adelta = 0;
+    if (a.dbg & 4)
+        ;
+    else if (push)
         cnt = gb_push_phase(nwords_u, ubits, prow, pcol, hubs, nhubs, H, mbits, mcomp,
                             (unsigned long long *)tbits, L, a.hprow, mfn, qbits, a.asg, adelta);
     else
@@ -1066,13 +1078,13 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
     if (gb_grid_sum(cnt, gst, &tot)) {
         *tcount = (unsigned long long)tot;
         if (a.iso_out) gb_iso_eval(a.mul, a.xcode, a.zcode, a.flip, a.a0, a.u0, a.iso_out);
-        if (a.pub) {  // hand the count to the host without a copy (gb_host_slot_wait)
+        if (a.pub && !(a.dbg & 1)) {  // hand the count to the host without a copy (gb_host_slot_wait)
             __hip_atomic_store(&a.pub->value, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __threadfence_system();
             __hip_atomic_store(&a.pub->seq, a.pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
-    if (a.mf_out) {
+    if (a.mf_out && !(a.dbg & 2)) {
         long long m;
         if (gb_grid_sum(mfn, gst + GB_GRID2_OFFSET, &m)) *a.mf_out = m;
     }
@@ -1244,6 +1256,8 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
                 args.asg_qiso_code = asg->q_iso_code;
                 args.asg_count = (unsigned long long *)asg->count;
             }
+            args.dbg = (int)gb_knob("iso_dbg");
+            if (args.dbg & 1) T.pub = nullptr;  // diagnostics: the host reads the count by a copy
             args.p1_steps = (int)gb_knob("pull_steps");
             if (args.p1_steps <= 0) args.p1_steps = 2;
             args.cap0 = (int)gb_knob("pull_cap");
