@@ -114,7 +114,7 @@ struct GB_Matrix_opaque {
     // (valid while pub_epoch == gb_epoch(): nothing enqueued since)
     struct gb_host_slot *pub;
     uint64_t pub_seq, pub_epoch;
-    // d_nvals[1] holds the edge count of this vector's entries in the rows of the
+    // d_nvals[2 .. 2 + GB_HINT_PARTS) hold (in parts) the edge count of this vector's entries in the rows of the
     // push-orientation CSR whose rowptr is hint_key (written by the BFS SpMV that
     // produced it; a stale hint only affects the push/pull choice, never results)
     bool hint_valid;
@@ -371,7 +371,7 @@ struct gb_vec_result {  // bitmap, type code ztype
     gb_host_slot *pub = nullptr;  // if set, the producing kernel publishes nvals here
     uint64_t pub_seq = 0;
     bool published = false;       // set by the producer when it did publish
-    const void *hint_key = nullptr;  // set when d_nvals[1] holds the edge-count hint
+    const void *hint_key = nullptr;  // set when d_nvals[2..] hold the edge-count hint parts
 };
 struct gb_mat_result {  // CSR
     int64_t nrows = 0, ncols = 0, nvals = 0;

@@ -657,7 +657,8 @@ struct gb_iso_args {
     int64_t spare_words;
     // pull shape: lane-per-row steps of 4 edges, then the first per-row cap of the list rounds
     int p1_steps, cap0;
-    int dbg;                        // diagnostics (knob iso_dbg): 1 no mailbox, 2 no hint sum, 4 no work
+    int dbg;                        // diagnostics (knob iso_dbg): 1 no mailbox, 2 no hint sum, 4 no work, 8 empty
+    bool packed;                    // one-round finish (iso_finish_packed): n < 2^27
     const uint64_t *rows_nonempty;  // pull rows with entries (nullptr: all)
     // fused deferred assign (gb_asg): w<q>(:) = x with q = u (asg.bits nullptr: none)
     gb_asg_dev asg;
@@ -1044,6 +1045,79 @@ __global__ void k_spmv_fold(SR sr, const int32_t *__restrict__ chunks, int64_t n
     gb_grid_add(cnt, tcount, gst);
 }
 
+// The result's finish in one round of atomics (n < 2^27): the block sums of the
+// count and of the fused assign's count delta travel packed in one 64-bit word
+// (arrival 10 bits | count 27 | delta 27) through the sharded grid sum, and the
+// next-frontier hint needs no root at all -- each shard's last block stores the
+// shard's total in the output's hint parts, which the hint's reader adds up.  All
+// of a block's atomics are issued together (one round trip instead of the six of
+// three separate grid sums: ~5 us per BFS level).
+#define ISO_ARR_BITS 10
+#define ISO_VAL_BITS 27
+__device__ __forceinline__ void iso_finish_packed(long long cnt, long long mfn, long long adelta,
+                                                  unsigned long long *__restrict__ tcount,
+                                                  unsigned long long *__restrict__ gst, const gb_iso_args &a) {
+    __shared__ long long part[3][SPMV_BLOCK / 64];
+    for (int off = 32; off > 0; off >>= 1) {
+        cnt += __shfl_xor(cnt, off, 64);
+        mfn += __shfl_xor(mfn, off, 64);
+        adelta += __shfl_xor(adelta, off, 64);
+    }
+    const int wid = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        part[0][wid] = cnt;
+        part[1][wid] = mfn;
+        part[2][wid] = adelta;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    cnt = mfn = adelta = 0;
+    for (int w = 0; w < SPMV_BLOCK / 64; w++) {
+        cnt += part[0][w];
+        mfn += part[1][w];
+        adelta += part[2][w];
+    }
+    const unsigned nb = gridDim.x;
+    const unsigned s = blockIdx.x % GB_GRID_SHARDS;
+    const unsigned in_shard = (nb - s + GB_GRID_SHARDS - 1) / GB_GRID_SHARDS;
+    const unsigned long long AM = (1ULL << ISO_ARR_BITS) - 1, VM = (1ULL << ISO_VAL_BITS) - 1;
+    unsigned long long *cs = gst + (size_t)s * GB_GRID_STRIDE;
+    unsigned long long *hs = gst + GB_GRID2_OFFSET + (size_t)s * GB_GRID_STRIDE;
+    const unsigned long long pk =
+        ((unsigned long long)adelta << (ISO_ARR_BITS + ISO_VAL_BITS)) | ((unsigned long long)cnt << ISO_ARR_BITS) | 1ULL;
+    unsigned long long oh = 0;
+    if (a.mf_out) {
+        oh = atomicAdd(hs, ((unsigned long long)mfn << 12) + 1ULL);
+        if (blockIdx.x == 0)  // the parts of shards no block maps to
+            for (unsigned i = nb; i < GB_HINT_PARTS; i++) a.mf_out[i] = 0;
+    }
+    const unsigned long long oc = atomicAdd(cs, pk);
+    if (a.mf_out && (unsigned)(oh & 0xFFF) + 1 == in_shard) {
+        a.mf_out[s] = (long long)(oh >> 12) + mfn;  // this shard's part of the hint
+        atomicExch(hs, 0ULL);
+    }
+    if ((unsigned)(oc & AM) + 1 != in_shard) return;
+    atomicExch(cs, 0ULL);
+    const unsigned long long scnt = ((oc >> ISO_ARR_BITS) & VM) + (unsigned long long)cnt;
+    const unsigned long long sadd = (oc >> (ISO_ARR_BITS + ISO_VAL_BITS)) + (unsigned long long)adelta;
+    const unsigned nshards = nb < GB_GRID_SHARDS ? nb : GB_GRID_SHARDS;
+    unsigned long long *root = gst + (size_t)GB_GRID_SHARDS * GB_GRID_STRIDE;
+    const unsigned long long o2 =
+        atomicAdd(root, (sadd << (ISO_ARR_BITS + ISO_VAL_BITS)) | (scnt << ISO_ARR_BITS) | 1ULL);
+    if ((unsigned)(o2 & AM) + 1 != nshards) return;
+    atomicExch(root, 0ULL);
+    const long long tot = (long long)(((o2 >> ISO_ARR_BITS) & VM) + scnt);
+    const long long add = (long long)((o2 >> (ISO_ARR_BITS + ISO_VAL_BITS)) + sadd);
+    *tcount = (unsigned long long)tot;
+    if (a.asg.bits && add) atomicAdd(a.asg_count, (unsigned long long)add);
+    if (a.iso_out) gb_iso_eval(a.mul, a.xcode, a.zcode, a.flip, a.a0, a.u0, a.iso_out);
+    if (a.pub && !(a.dbg & 1)) {  // hand the count to the host without a copy (gb_host_slot_wait)
+        __hip_atomic_store(&a.pub->value, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+        __hip_atomic_store(&a.pub->seq, a.pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // One launch does the chosen direction and finishes the result: count
 // (stored, no prior zeroing needed), next-frontier hint, iso value, mailbox.
 __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
@@ -1054,8 +1128,13 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
     unsigned long long *__restrict__ tcount, unsigned long long *__restrict__ gst, gb_iso_args a) {
     __shared__ gb_wlist lists[WAVES_PER_BLOCK];
     gb_wlist &L = lists[threadIdx.x >> 6];
+    if (a.dbg & 8) return;  // diagnostics: the launch alone
     bool push = false;
-    if (a.mf_hint) push = gb_dir_decide(*a.mf_hint, a.rule);
+    if (a.mf_hint) {
+        long long mf = 0;  // the hint's parts (one per grid-sum shard of its producer)
+        for (int i = 0; i < GB_HINT_PARTS; i++) mf += a.mf_hint[i];
+        push = gb_dir_decide(mf, a.rule);
+    }
     else if (a.dst) push = a.dst[ST_PUSH] != 0;
     if (a.spare) {
         for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < a.spare_words;
@@ -1074,6 +1153,10 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
     else
         cnt = gb_pull_iso_phase(nrows, rowptr, colidx, ubits, mbits, mcomp, tbits, L, a.hprow, mfn, a.p1_steps,
                                 a.cap0, a.rows_nonempty, qbits, a.asg, adelta);
+    if (a.packed) {
+        iso_finish_packed(cnt, mfn, adelta, tcount, gst, a);
+        return;
+    }
     long long tot;
     if (gb_grid_sum(cnt, gst, &tot)) {
         *tcount = (unsigned long long)tot;
@@ -1086,7 +1169,10 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
     }
     if (a.mf_out && !(a.dbg & 2)) {
         long long m;
-        if (gb_grid_sum(mfn, gst + GB_GRID2_OFFSET, &m)) *a.mf_out = m;
+        if (gb_grid_sum(mfn, gst + GB_GRID2_OFFSET, &m)) {
+            a.mf_out[0] = m;
+            for (int i = 1; i < GB_HINT_PARTS; i++) a.mf_out[i] = 0;
+        }
     }
     if (a.asg.bits) gb_grid_add(adelta, a.asg_count, gst + GB_GRID3_OFFSET);
 }
@@ -1229,7 +1315,8 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
     T.iso = iso;
     T.bits = gb_malloc_n<uint64_t>(gb_words(n));
     T.dense = gb_malloc((iso ? 1 : n) * zs);
-    T.d_nvals = gb_malloc_n<int64_t>(2);  // [1]: next-frontier edge hint (iso path)
+    // [0] count; [2 .. 2 + GB_HINT_PARTS): next-frontier edge hint in parts (iso path)
+    T.d_nvals = gb_malloc_n<int64_t>(2 + GB_HINT_PARTS);
     if (n == 0) {
         gb_memset(T.d_nvals, 0, sizeof(int64_t));
         return;
@@ -1263,9 +1350,11 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
                 args.asg_count = (unsigned long long *)asg->count;
             }
             args.dbg = (int)gb_knob("iso_dbg");
+            args.packed = n < (1LL << ISO_VAL_BITS) && u.n < (1LL << ISO_VAL_BITS) && gb_knob("iso_packed") != 1;
             if (args.dbg & 1) T.pub = nullptr;  // diagnostics: the host reads the count by a copy
-            args.p1_steps = (int)gb_knob("pull_steps");
-            if (args.p1_steps <= 0) args.p1_steps = 2;
+            args.p1_steps = (int)gb_knob("pull_steps");  // -1: no lane-per-row steps
+            if (args.p1_steps == 0) args.p1_steps = 2;
+            if (args.p1_steps < 0) args.p1_steps = 0;
             args.cap0 = (int)gb_knob("pull_cap");
             if (args.cap0 <= 0) args.cap0 = 16;
             args.rows_nonempty = A.nonempty;
@@ -1298,7 +1387,7 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
                 units = std::max<int64_t>(units, std::max<int64_t>((Apush->nhubs + 15) / 16, (uw + 3) / 4));
                 if (n == u.n) {  // outputs index the same vertex space as u: they can seed the next call
                     args.hprow = Apush->rowptr;
-                    args.mf_out = (long long *)(T.d_nvals + 1);
+                    args.mf_out = (long long *)(T.d_nvals + 2);
                     T.hint_key = Apush->rowptr;
                 }
                 const bool hint_ok = u.mf_hint && u.hint_key == Apush->rowptr;
@@ -1343,6 +1432,7 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             int64_t gcap = gb_knob("iso_work_grid");
             if (gcap <= 0) gcap = iso_work_resident_blocks();
             const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 3) / 4, gcap));
+            if (grid >= GB_GRID_SHARDS * ((1u << ISO_ARR_BITS) - 1)) args.packed = false;  // arrival field
             hipLaunchKernelGGL(k_iso_work, dim3(grid), dim3(SPMV_BLOCK), 0, gb_stream(), n, A.rowptr, A.colidx, uw,
                                u.bits, can_push ? Apush->rowptr : nullptr, can_push ? Apush->colidx : nullptr,
                                can_push ? Apush->hubs : nullptr, can_push ? Apush->nhubs : 0,

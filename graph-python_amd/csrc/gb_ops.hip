@@ -67,7 +67,7 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
     gb_bitmap_view uv;
     gb_get_bitmap(uv, u);
     if (u->kind != GB_KIND_MATRIX && u->hint_valid) {
-        uv.mf_hint = (const long long *)(u->d_nvals + 1);
+        uv.mf_hint = (const long long *)(u->d_nvals + 2);  // GB_HINT_PARTS parts
         uv.hint_key = u->hint_key;
     }
     gb_vmask m;

@@ -9,3 +9,4 @@
 #define GB_GRID2_OFFSET (GB_GRID_STATE_WORDS + 32)  // a second grid-sum area (two sums in one kernel)
 #define GB_GRID3_OFFSET (GB_GRID2_OFFSET + GB_GRID_STATE_WORDS)  // a third one
 #define GB_STATE_WORDS (GB_GRID3_OFFSET + GB_GRID_STATE_WORDS)
+#define GB_HINT_PARTS GB_GRID_SHARDS  // parts of a vector's next-frontier edge hint (d_nvals[2..])
