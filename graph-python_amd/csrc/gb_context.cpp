@@ -160,11 +160,22 @@ int64_t gb_knob(const char *key) {
 // 10 us of host time each, measured in profiles/) off the per-call path.
 namespace {
 std::mutex g_mem_mu;
-std::unordered_map<void *, size_t> g_live;           // ptr -> class size
-std::unordered_map<size_t, std::vector<void *>> g_cache;  // class size -> idle blocks
+struct gb_cached {
+    void *p;
+    uint64_t seq;  // free order (eviction oldest first)
+};
+std::unordered_map<void *, size_t> g_live;                    // ptr -> class size
+std::unordered_map<size_t, std::vector<gb_cached>> g_cache;  // class size -> idle blocks
+std::map<uint64_t, std::pair<void *, size_t>> g_lru;          // seq -> (ptr, class)
+uint64_t g_free_seq = 0;
 size_t g_cached_bytes = 0;
-const size_t kCacheLimit = (size_t)32 << 30;  // idle bytes kept (of 288 GB HBM)
-void *g_pinned = nullptr;                     // pinned staging for small device->host reads
+// Idle bytes kept (of 288 GB HBM).  A block freed over the limit evicts the
+// oldest idle blocks rather than being dropped itself: the blocks of the work
+// that is running now are the ones the next call asks for again (a 42 GB
+// SpGEMM output handed back to the pool and requested again after a run of
+// other sizes was split by them and re-mapped fresh: ~2 s per call).
+const size_t kCacheLimit = (size_t)96 << 30;
+void *g_pinned = nullptr;  // pinned staging for small device->host reads
 const size_t kPinned = 1 << 16;
 std::mutex g_pin_mu;
 
@@ -181,9 +192,25 @@ size_t size_class(size_t b) {
 
 void release_cache_locked() {
     for (auto &kv : g_cache)
-        for (void *p : kv.second) (void)hipFreeAsync(p, gb_stream());
+        for (const gb_cached &c : kv.second) (void)hipFreeAsync(c.p, gb_stream());
     g_cache.clear();
+    g_lru.clear();
     g_cached_bytes = 0;
+}
+
+void evict_oldest_locked() {
+    auto it = g_lru.begin();
+    void *p = it->second.first;
+    const size_t cls = it->second.second;
+    g_lru.erase(it);
+    auto &v = g_cache[cls];
+    for (size_t i = 0; i < v.size(); i++)
+        if (v[i].p == p) {
+            v.erase(v.begin() + (std::ptrdiff_t)i);
+            break;
+        }
+    g_cached_bytes -= cls;
+    (void)hipFreeAsync(p, gb_stream());
 }
 }  // namespace
 
@@ -192,11 +219,12 @@ void *gb_malloc(size_t bytes) {
     std::lock_guard<std::mutex> lk(g_mem_mu);
     auto it = g_cache.find(cls);
     if (it != g_cache.end() && !it->second.empty()) {
-        void *p = it->second.back();
+        const gb_cached c = it->second.back();
         it->second.pop_back();
+        g_lru.erase(c.seq);
         g_cached_bytes -= cls;
-        g_live[p] = cls;
-        return p;
+        g_live[c.p] = cls;
+        return c.p;
     }
     void *p = nullptr;
     hipError_t e = hipMallocAsync(&p, cls, gb_stream());
@@ -224,12 +252,15 @@ void gb_free(void *p) {
     }
     size_t cls = it->second;
     g_live.erase(it);
-    if (g_cached_bytes + cls <= kCacheLimit) {
-        g_cache[cls].push_back(p);
-        g_cached_bytes += cls;
-    } else {
+    if (cls > kCacheLimit) {
         (void)hipFreeAsync(p, gb_stream());
+        return;
     }
+    while (g_cached_bytes + cls > kCacheLimit && !g_lru.empty()) evict_oldest_locked();
+    const uint64_t seq = ++g_free_seq;
+    g_cache[cls].push_back(gb_cached{p, seq});
+    g_lru.emplace(seq, std::make_pair(p, cls));
+    g_cached_bytes += cls;
 }
 
 void gb_memset(void *p, int v, size_t bytes) {

@@ -99,6 +99,18 @@ DESCS = {
 }
 
 
+
+def _write_if_changed(path, text):
+    """Leave an unchanged file alone so make does not rebuild everything that includes it."""
+    try:
+        with open(path) as f:
+            if f.read() == text:
+                return
+    except FileNotFoundError:
+        pass
+    with open(path, "w") as f:
+        f.write(text)
+
 def binop_table():
     """-> list of (name, opcode name, xtype, ztype); xtype None = positional."""
     out = []
@@ -253,8 +265,7 @@ def main():
         lines.append(f"    GBAMD_MON_{n} = {i},\n")
     lines.append(f"    GBAMD_MON_COUNT = {len(MONOIDS)}\n}};\n")
     lines.append("#endif\n")
-    with open(os.path.join(ROOT, "include", "gbamd_codes.h"), "w") as f:
-        f.write("".join(lines))
+    _write_if_changed(os.path.join(ROOT, "include", "gbamd_codes.h"), "".join(lines))
 
     # ---------------- extern declarations
     d = [HEADER_NOTE, "#ifndef GRAPHBLAS_AMD_BUILTINS_H\n#define GRAPHBLAS_AMD_BUILTINS_H\n"]
@@ -279,8 +290,7 @@ def main():
     for name in DESCS.values():
         d.append(f"GB_EXTERN GrB_Descriptor {name};\n")
     d.append("#endif\n")
-    with open(os.path.join(ROOT, "include", "graphblas_amd_builtins.h"), "w") as f:
-        f.write("".join(d))
+    _write_if_changed(os.path.join(ROOT, "include", "graphblas_amd_builtins.h"), "".join(d))
 
     # ---------------- definitions
     c = [HEADER_NOTE, '#include "gb_internal.h"\n\n']
@@ -334,8 +344,7 @@ def main():
     for u in unops:
         c.append(f"    {{\"{u[0]}\", 5, (void*)&U_{u[0]}}},\n")
     c.append("    {nullptr, -1, nullptr}\n};\n")
-    with open(os.path.join(ROOT, "graph-python_amd", "csrc", "gb_builtins.cpp"), "w") as f:
-        f.write("".join(c))
+    _write_if_changed(os.path.join(ROOT, "graph-python_amd", "csrc", "gb_builtins.cpp"), "".join(c))
 
     # ---------------- python table
     p = ['"""GENERATED by tools/gen_builtins.py -- do not edit.\n\n'
@@ -360,8 +369,7 @@ def main():
     for k, v in DESCS.items():
         p.append(f"    {k!r}: {v!r},\n")
     p.append("}\n")
-    with open(os.path.join(ROOT, "graph-python_amd", "graphblas_amd", "_builtins.py"), "w") as f:
-        f.write("".join(p))
+    _write_if_changed(os.path.join(ROOT, "graph-python_amd", "graphblas_amd", "_builtins.py"), "".join(p))
     print(f"types={len(TYPES)} binops={len(binops)} unops={len(unops)} monoids={len(monoids)} "
           f"semirings={len(semirings)} (+{sum(len(s[3]) for s in semirings)} aliases) "
           f"descriptors={len(DESCS)}")
