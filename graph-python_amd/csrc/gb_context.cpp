@@ -21,6 +21,7 @@ hipStream_t g_user_stream = nullptr;
 bool g_user_stream_set = false;
 std::mutex g_knob_mu;
 std::map<std::string, int64_t> g_knobs;
+std::atomic<bool> g_any_knob{false};  // no knob ever set: every lookup is 0 without the lock
 }  // namespace
 
 static const GrB_Index GB_ALL_SENTINEL = 0;
@@ -148,6 +149,7 @@ unsigned long long *gb_device_state() {
 }
 
 int64_t gb_knob(const char *key) {
+    if (!g_any_knob.load(std::memory_order_acquire)) return 0;
     std::lock_guard<std::mutex> lk(g_knob_mu);
     auto it = g_knobs.find(key);
     return it == g_knobs.end() ? 0 : it->second;
@@ -372,6 +374,7 @@ GrB_Info GxB_Global_set_int(const char *key, int64_t value) {
     if (!key) return GrB_NULL_POINTER;
     std::lock_guard<std::mutex> lk(g_knob_mu);
     g_knobs[key] = value;
+    g_any_knob.store(true, std::memory_order_release);
     return GrB_SUCCESS;
 }
 

@@ -236,6 +236,7 @@ struct gb_wlist {
     int32_t pref[WL_MAX]; // inclusive prefix of this round's lengths
     int16_t id[WL_MAX];   // u * 64 + lane of the row (pull)
     int8_t hit[WL_MAX];   // a k present in u was found this round
+    unsigned long long hitw[PULL_U];  // pull: rows of the unit's words found through the list
 };
 
 // this round takes min(rem[i], cap) edges of segment i; hit[i] = 0; pref = inclusive
@@ -430,7 +431,7 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
                                                       const int64_t *__restrict__ hprow, long long &mfn,
                                                       int p1_steps, int cap0, const uint64_t *__restrict__ rne,
                                                       const uint64_t *__restrict__ qbits, const gb_asg_dev &g,
-                                                      long long &adelta) {
+                                                      long long &adelta, int dbg = 0) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -497,8 +498,13 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
             for (int u = 0; u < PULL_U; u++) {
                 if (go[u]) {
                     int f = 0;
+                    if (dbg & 32) {  // diagnostics: no frontier probes in the steps
 #pragma unroll
-                    for (int t = 0; t < 4; t++) f += k[u][t] >= 0 && gb_bit(ubits, k[u][t]);
+                        for (int t = 0; t < 4; t++) f += k[u][t] == 0x7fffffff;
+                    } else {
+#pragma unroll
+                        for (int t = 0; t < 4; t++) f += k[u][t] >= 0 && gb_bit(ubits, k[u][t]);
+                    }
                     found[u] = f != 0;
                     p[u] += 4;
                 }
@@ -518,9 +524,8 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
             }
             n += __popcll(bb);
         }
-        unsigned long long hitw[PULL_U];
-#pragma unroll
-        for (int u = 0; u < PULL_U; u++) hitw[u] = 0;
+        if (lane < PULL_U) L.hitw[lane] = 0;
+        if (dbg & 16) n = 0;  // diagnostics: rows left after the steps are dropped
         int cap = cap0;
         while (n) {
             gb_wave_sync();
@@ -560,19 +565,7 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
                     nr = L.rem[i] - taken;
                     alive = !hit && nr > 0;
                 }
-#pragma unroll
-                for (int u = 0; u < PULL_U; u++) {
-                    const unsigned long long hb = __ballot(hit && (id >> 6) == u);
-                    // lane `id & 63` of word u found a k: collect the bits by row lane
-                    unsigned long long bits = 0;
-                    unsigned long long t = hb;
-                    while (t) {
-                        const int l = __ffsll(t) - 1;
-                        t &= t - 1;
-                        bits |= 1ULL << (__shfl((int)id, l, 64) & 63);
-                    }
-                    hitw[u] |= bits;
-                }
+                if (hit) atomicOr(&L.hitw[id >> 6], 1ULL << (id & 63));
                 const unsigned long long ab = __ballot(alive);
                 gb_wave_sync();
                 if (alive) {
@@ -587,9 +580,10 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
             n = m;
             cap = cap < (1 << 20) ? cap * 2 : cap;
         }
+        gb_wave_sync();
 #pragma unroll
         for (int u = 0; u < PULL_U; u++) {
-            if ((hitw[u] >> lane) & 1ULL) found[u] = true;
+            if ((L.hitw[u] >> lane) & 1ULL) found[u] = true;
             const unsigned long long word = __ballot(found[u]);
             if (lane == 0 && w0 + u < nwords) {
                 tbits[w0 + u] = word;
@@ -657,7 +651,8 @@ struct gb_iso_args {
     int64_t spare_words;
     // pull shape: lane-per-row steps of 4 edges, then the first per-row cap of the list rounds
     int p1_steps, cap0;
-    int dbg;                        // diagnostics (knob iso_dbg): 1 no mailbox, 2 no hint sum, 4 no work, 8 empty
+    int dbg;                        // diagnostics (knob iso_dbg): 1 no mailbox, 2 no hint sum, 4 no work, 8 empty,
+                                    // 16 pull without its segment list, 32 pull steps without probes (wrong results)
     bool packed;                    // one-round finish (iso_finish_packed): n < 2^27
     const uint64_t *rows_nonempty;  // pull rows with entries (nullptr: all)
     // fused deferred assign (gb_asg): w<q>(:) = x with q = u (asg.bits nullptr: none)
@@ -1152,7 +1147,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
                             (unsigned long long *)tbits, L, a.hprow, mfn, qbits, a.asg, adelta);
     else
         cnt = gb_pull_iso_phase(nrows, rowptr, colidx, ubits, mbits, mcomp, tbits, L, a.hprow, mfn, a.p1_steps,
-                                a.cap0, a.rows_nonempty, qbits, a.asg, adelta);
+                                a.cap0, a.rows_nonempty, qbits, a.asg, adelta, a.dbg);
     if (a.packed) {
         iso_finish_packed(cnt, mfn, adelta, tcount, gst, a);
         return;

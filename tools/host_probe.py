@@ -14,6 +14,9 @@ import graphblas_amd as gb  # noqa: E402
 
 scale = int(sys.argv[1]) if len(sys.argv) > 1 else 22
 lib = gb.lib
+for kv in sys.argv[2:]:  # library knobs k=v
+    k_, v_ = kv.split("=")
+    gb.set_knob(k_, int(v_))
 stream = torch.cuda.Stream()
 gb.set_stream(stream)
 n = 1 << scale
