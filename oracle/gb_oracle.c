@@ -659,6 +659,92 @@ int or_bfs_levels(const or_csr *A, int64_t src, int32_t *levels, int64_t *edges)
     return lev;
 }
 
+/* The same level BFS as or_bfs_levels -- per level q(~v.S, replace) = q lor.land A,
+ * the masked vxm of the reference notebook loop (Example B.1 cell 8) -- run on
+ * `nthreads` host threads the way a CPU GraphBLAS library runs a masked vxm with
+ * a bitmap frontier: push (saxpy over the frontier's rows of A) or pull (dot over
+ * the unvisited rows of A^T, stopping at the first frontier hit), chosen per level
+ * by Beamer's rule (frontier edges x 14 > unvisited edges -> pull).  CPU BASELINE
+ * ONLY (bench.py cpu_baseline); same levels as or_bfs_levels. */
+int or_bfs_levels_par(const or_csr *A, const or_csr *AT, int64_t src, int32_t *levels, int64_t *edges,
+                      int nthreads) {
+    const int64_t n = A->nrows, nw = (n + 63) / 64, nnz = A->p[n];
+    if (nthreads < 1) nthreads = 1;
+    int64_t *q = (int64_t *)xmalloc((size_t)(n ? n : 1) * sizeof(int64_t));
+    int64_t *nq = (int64_t *)xmalloc((size_t)(n ? n : 1) * sizeof(int64_t));
+    uint64_t *fb = (uint64_t *)calloc((size_t)(nw ? nw : 1), sizeof(uint64_t));
+    memset(levels, 0, (size_t)n * sizeof(int32_t));
+    int64_t qn = 1, e = 0, open_edges = nnz;
+    int lev = 1;
+    q[0] = src; levels[src] = 1;
+    while (qn > 0) {
+        int64_t mf = 0;
+#pragma omp parallel for num_threads(nthreads) reduction(+ : mf) schedule(static)
+        for (int64_t a = 0; a < qn; a++) mf += A->p[q[a] + 1] - A->p[q[a]];
+        e += mf;
+        open_edges -= mf;
+        const int pull = AT && mf * 14 > open_edges;
+        int64_t nn = 0;
+        if (pull) {
+#pragma omp parallel for num_threads(nthreads) schedule(static)
+            for (int64_t a = 0; a < qn; a++)
+                __atomic_fetch_or(&fb[q[a] >> 6], 1ULL << (q[a] & 63), __ATOMIC_RELAXED);
+#pragma omp parallel num_threads(nthreads)
+            {
+                int64_t cap = 4096, cnt = 0;
+                int64_t *buf = (int64_t *)xmalloc((size_t)cap * sizeof(int64_t));
+#pragma omp for schedule(dynamic, 4096) nowait
+                for (int64_t w = 0; w < n; w++) {
+                    if (levels[w]) continue;
+                    for (int64_t p = AT->p[w]; p < AT->p[w + 1]; p++) {
+                        const int64_t k = AT->j[p];
+                        if ((fb[k >> 6] >> (k & 63)) & 1) {
+                            if (cnt == cap) buf = (int64_t *)realloc(buf, (size_t)(cap *= 2) * sizeof(int64_t));
+                            buf[cnt++] = w;
+                            break;
+                        }
+                    }
+                }
+                const int64_t at = __atomic_fetch_add(&nn, cnt, __ATOMIC_RELAXED);
+                memcpy(nq + at, buf, (size_t)cnt * sizeof(int64_t));
+                free(buf);
+            }
+#pragma omp parallel for num_threads(nthreads) schedule(static)
+            for (int64_t a = 0; a < qn; a++) fb[q[a] >> 6] = 0;
+#pragma omp parallel for num_threads(nthreads) schedule(static)
+            for (int64_t a = 0; a < nn; a++) levels[nq[a]] = lev + 1;
+        } else {
+#pragma omp parallel num_threads(nthreads)
+            {
+                int64_t cap = 4096, cnt = 0;
+                int64_t *buf = (int64_t *)xmalloc((size_t)cap * sizeof(int64_t));
+#pragma omp for schedule(dynamic, 16) nowait
+                for (int64_t a = 0; a < qn; a++) {
+                    const int64_t v = q[a];
+                    for (int64_t p = A->p[v]; p < A->p[v + 1]; p++) {
+                        const int64_t w = A->j[p];
+                        int32_t zero = 0;
+                        if (!__atomic_load_n(&levels[w], __ATOMIC_RELAXED) &&
+                            __atomic_compare_exchange_n(&levels[w], &zero, lev + 1, 0, __ATOMIC_RELAXED,
+                                                        __ATOMIC_RELAXED)) {
+                            if (cnt == cap) buf = (int64_t *)realloc(buf, (size_t)(cap *= 2) * sizeof(int64_t));
+                            buf[cnt++] = w;
+                        }
+                    }
+                }
+                const int64_t at = __atomic_fetch_add(&nn, cnt, __ATOMIC_RELAXED);
+                memcpy(nq + at, buf, (size_t)cnt * sizeof(int64_t));
+                free(buf);
+            }
+        }
+        int64_t *t = q; q = nq; nq = t; qn = nn;
+        if (qn) lev++;
+    }
+    free(q); free(nq); free(fb);
+    if (edges) *edges = e;
+    return lev;
+}
+
 /* Level BFS exactly as the reference notebook loop (Example B.1 cell 8), every
  * step through or_mxm:  v[:](mask=q.V) << d ; q(~v.S, replace) << q.vxm(A, lor_land).
  * This is the CPU baseline "port" of the GraphBLAS formulation. */

@@ -277,6 +277,17 @@ def bfs_levels(A, src):
     return lev, nl, edges.value
 
 
+def bfs_levels_par(A, AT, src, nthreads):
+    """or_bfs_levels on nthreads host threads (push/pull per level); AT = A^T or None."""
+    lev = np.zeros(A.nrows, np.int32)
+    edges = ctypes.c_int64(0)
+    cat = AT._c() if AT is not None else None
+    nl = lib().or_bfs_levels_par(ctypes.byref(A._c()), ctypes.byref(cat) if cat is not None else None,
+                                 ctypes.c_int64(src), lev.ctypes.data_as(ctypes.c_void_p), ctypes.byref(edges),
+                                 ctypes.c_int(nthreads))
+    return lev, nl, edges.value
+
+
 def bfs_graphblas(A, src):
     """The Level-BFS loop of the reference notebook (Example B.1 cell 8) through or_mxm:
        v[:](mask=q.V) << d ; q(~v.S, replace) << q.vxm(A, lor_land) ; stop when q empty."""
