@@ -55,7 +55,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-secondary", action="store_true", help="skip the config 2 / config 4 lines")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
-    p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     # rehearsal of the N>1 path on one GPU: all ranks on one device, gloo transport
     p.add_argument("--dist-backend", default="nccl")
     p.add_argument("--device", type=int, default=None, help="override LOCAL_RANK's device")
