@@ -28,6 +28,7 @@
 // Work is sum over mask entries of min(|A'(i,:)|, |B'^T(j,:)|) streamed keys
 // plus one LDS search each -- instead of a search in global memory per key.
 #include <algorithm>
+#include <cstdio>
 
 #include "gb_dispatch.cuh"
 #include "gb_internal.h"
@@ -71,10 +72,11 @@ __device__ __forceinline__ bool dt_side_of(int64_t a, int64_t b) {
 
 // ---------------------------------------------------------------- classify
 // flags (pre-zeroed): tflag[p] = 1 for this phase's entries of task-sized groups
-// (G order); hflag[q] = 1 for entries whose longer list exceeds DT_CAP (CSR order)
+// (G order); entries whose longer list exceeds the cap: hg[p] = 1 (G order) when
+// they run as pieces, else hflag[q] = 1 (CSR order, the per-entry wave kernel)
 template <bool SWAP>
 __global__ __launch_bounds__(DT_BLOCK) void k_dt_classify(dt_side s, int cap, uint8_t *__restrict__ tflag,
-                                                         uint8_t *__restrict__ hflag) {
+                                                         uint8_t *__restrict__ hflag, uint8_t *__restrict__ hg) {
     const int lane = threadIdx.x & 63;
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
     for (int64_t g = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; g < s.ng; g += nw) {
@@ -85,22 +87,26 @@ __global__ __launch_bounds__(DT_BLOCK) void k_dt_classify(dt_side s, int cap, ui
             const int64_t b = s.yrp[o + 1] - s.yrp[o];
             if (b == 0 || !dt_side_of<SWAP>(a, b)) continue;  // an empty Y list matches nothing
             if (a <= cap) tflag[p] = 1;
+            else if (hg) hg[p] = 1;  // pieces (G order)
             else hflag[s.perm ? s.perm[p] : p] = 1;
         }
     }
 }
 
 // compacted task entries in G order: group, Y start and length, other index, CSR slot
+// (huge: the entries of groups longer than the cap, and the longest such group in *amax)
 template <bool SWAP>
 __global__ __launch_bounds__(DT_BLOCK) void k_dt_compact(dt_side s, int cap, const uint8_t *__restrict__ tflag,
                                                         const int64_t *__restrict__ pos, int32_t *__restrict__ eG,
                                                         int64_t *__restrict__ eYS, int32_t *__restrict__ eO,
-                                                        int32_t *__restrict__ eB, int64_t *__restrict__ eQ) {
+                                                        int32_t *__restrict__ eB, int64_t *__restrict__ eQ, bool huge,
+                                                        unsigned long long *__restrict__ amax) {
     const int lane = threadIdx.x & 63;
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
     for (int64_t g = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; g < s.ng; g += nw) {
         const int64_t a = s.xrp[g + 1] - s.xrp[g];
-        if (a <= DT_MID || a > cap) continue;
+        if (huge ? a <= cap : (a <= DT_MID || a > cap)) continue;
+        if (huge && lane == 0) atomicMax(amax, (unsigned long long)a);
         for (int64_t p = s.grp_rp[g] + lane; p < s.grp_rp[g + 1]; p += 64) {
             if (!tflag[p]) continue;
             const int32_t o = s.grp_oi[p];
@@ -113,6 +119,72 @@ __global__ __launch_bounds__(DT_BLOCK) void k_dt_compact(dt_side s, int cap, con
             eQ[e] = s.perm ? s.perm[p] : p;
         }
     }
+}
+
+// Pieces of the longest lists (> cap keys): piece j of X(g,:) is its keys
+// [j * cap, (j + 1) * cap).  An entry's work in piece j is the run of its Y keys
+// inside the piece's key range (found by two binary searches), cut into sub-entries
+// of at most cap keys (the task kernel's flat-space bound); cnt[i] = number of them.
+__device__ __forceinline__ int64_t dt_lower(const int32_t *__restrict__ v, int64_t lo, int64_t hi, int32_t k) {
+    while (lo < hi) {
+        const int64_t m = (lo + hi) >> 1;
+        if (v[m] < k) lo = m + 1;
+        else hi = m;
+    }
+    return lo;
+}
+
+__global__ void k_dt_piece_flags(dt_side s, int64_t nh, int piece, int cap, const int32_t *__restrict__ hG,
+                                 const int64_t *__restrict__ hYS, const int32_t *__restrict__ hB,
+                                 uint8_t *__restrict__ cnt, int64_t *__restrict__ pys, int32_t *__restrict__ pb) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nh; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t g = hG[i], xs = s.xrp[g], a = s.xrp[g + 1] - xs, x0 = (int64_t)piece * cap;
+        uint8_t c = 0;
+        if (x0 < a) {
+            const int64_t x1 = (x0 + cap < a ? x0 + cap : a) - 1;
+            const int32_t k0 = s.xci[xs + x0], k1 = s.xci[xs + x1];
+            const int64_t ys = hYS[i], ye = ys + hB[i];
+            const int64_t lo = dt_lower(s.yci, ys, ye, k0);
+            const int64_t hi = k1 == INT32_MAX ? ye : dt_lower(s.yci, lo, ye, k1 + 1);
+            pys[i] = lo;
+            pb[i] = (int32_t)(hi - lo);
+            c = (uint8_t)((hi - lo + cap - 1) / cap);
+        }
+        cnt[i] = c;
+    }
+}
+
+__global__ void k_dt_piece_compact(int64_t nh, int cap, const uint8_t *__restrict__ cnt,
+                                   const int64_t *__restrict__ pos, const int32_t *__restrict__ hG,
+                                   const int32_t *__restrict__ hO, const int64_t *__restrict__ hQ,
+                                   const int64_t *__restrict__ pys, const int32_t *__restrict__ pb,
+                                   int32_t *__restrict__ eG, int64_t *__restrict__ eYS, int32_t *__restrict__ eO,
+                                   int32_t *__restrict__ eB, int64_t *__restrict__ eQ) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nh; i += (int64_t)gridDim.x * blockDim.x) {
+        for (int c = 0; c < cnt[i]; c++) {
+            const int64_t e = pos[i] + c;
+            const int64_t o0 = (int64_t)c * cap;
+            eG[e] = hG[i];
+            eYS[e] = pys[i] + o0;
+            eO[e] = hO[i];
+            eB[e] = (int32_t)(pb[i] - o0 < cap ? pb[i] - o0 : cap);
+            eQ[e] = hQ[i];
+        }
+    }
+}
+
+// huge entries left to the per-entry kernel: G-order flags -> CSR-order flags
+__global__ void k_dt_huge_to_csr(int64_t nm, const uint8_t *__restrict__ hg, const int64_t *__restrict__ perm,
+                                 uint8_t *__restrict__ hflag) {
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < nm; p += (int64_t)gridDim.x * blockDim.x)
+        if (hg[p]) hflag[perm ? perm[p] : p] = 1;
+}
+
+// the huge entries' outputs start at the monoid identity (pieces fold into them)
+template <class Z>
+__global__ void k_dt_ident(int64_t nh, const int64_t *__restrict__ hQ, Z *__restrict__ tval, Z ident) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nh; i += (int64_t)gridDim.x * blockDim.x)
+        tval[hQ[i]] = ident;
 }
 
 // a task starts where the group changes or the cost prefix enters a new window
@@ -306,6 +378,44 @@ constexpr int DT_FLOG = 18;      // filter bits (log2)
 
 __device__ __forceinline__ uint32_t dt_hash(int32_t k) { return ((uint32_t)k * 0x9E3779B1u) >> (32 - DT_FLOG); }
 
+// fold z into T's 4- or 8-byte output slot (pieces of one entry meet here; exact monoids)
+template <class SR, class Z>
+__device__ __forceinline__ void dt_global_fold(const SR &sr, bool any_store, Z *slot, Z z) {
+    if (any_store) {
+        *slot = z;
+    } else if constexpr (std::is_same<SR, gb_sr_min_plus<int64_t>>::value) {
+        atomicMin((long long *)slot, (long long)z);
+    } else if constexpr (sizeof(Z) == 8) {
+        unsigned long long *w = (unsigned long long *)slot;
+        unsigned long long old = *(volatile unsigned long long *)w;
+        while (true) {
+            Z cur;
+            __builtin_memcpy(&cur, &old, 8);
+            const Z nv = sr.add(cur, z);
+            unsigned long long nb;
+            __builtin_memcpy(&nb, &nv, 8);
+            if (nb == old) return;
+            const unsigned long long prev = atomicCAS(w, old, nb);
+            if (prev == old) return;
+            old = prev;
+        }
+    } else if constexpr (sizeof(Z) == 4) {
+        unsigned int *w = (unsigned int *)slot;
+        unsigned int old = *(volatile unsigned int *)w;
+        while (true) {
+            Z cur;
+            __builtin_memcpy(&cur, &old, 4);
+            const Z nv = sr.add(cur, z);
+            unsigned int nb;
+            __builtin_memcpy(&nb, &nv, 4);
+            if (nb == old) return;
+            const unsigned int prev = atomicCAS(w, old, nb);
+            if (prev == old) return;
+            old = prev;
+        }
+    }
+}
+
 template <class SR, class Z>
 __device__ __forceinline__ void dt_slot_fold(const SR &sr, bool any_store, unsigned long long *slot, Z z) {
     if (any_store) {
@@ -322,7 +432,8 @@ __global__ __launch_bounds__(DT_TB) void k_dot_task(
     SR sr, int mon, dt_side s, const X *__restrict__ xvx, bool x_iso, const X *__restrict__ yvx, bool y_iso,
     int64_t ntask, const int64_t *__restrict__ tstart, const int32_t *__restrict__ eG,
     const int64_t *__restrict__ eYS, const int32_t *__restrict__ eO, const int32_t *__restrict__ eB,
-    const int64_t *__restrict__ eQ, Z *__restrict__ tval, uint8_t *__restrict__ tflag, int dbg) {
+    const int64_t *__restrict__ eQ, Z *__restrict__ tval, uint8_t *__restrict__ tflag, int dbg, int piece,
+    int pcap) {
     __shared__ int32_t keys[DT_CAP];
     __shared__ uint32_t filt[1 << (DT_FLOG - 5)];
     __shared__ uint64_t estart[DT_SMAX / 64 + 1];     // bit f: an entry starts at flat element f
@@ -347,8 +458,14 @@ __global__ __launch_bounds__(DT_TB) void k_dot_task(
         const int64_t e0 = tstart[t];
         const int ne = __builtin_amdgcn_readfirstlane((int)(tstart[t + 1] - e0));
         const int64_t g = eG[e0];
-        const int64_t xs = s.xrp[g];
-        const int a = __builtin_amdgcn_readfirstlane((int)(s.xrp[g + 1] - xs));
+        int64_t xs = s.xrp[g];
+        int64_t alen = s.xrp[g + 1] - xs;
+        if (piece >= 0) {  // piece `piece` of a list longer than the cap
+            xs += (int64_t)piece * pcap;
+            alen -= (int64_t)piece * pcap;
+            if (alen > pcap) alen = pcap;
+        }
+        const int a = __builtin_amdgcn_readfirstlane((int)alen);
         for (int i = tid; i < (1 << (DT_FLOG - 5)); i += DT_TB) filt[i] = 0;
         for (int i = tid; i < DT_SMAX / 64 + 1; i += DT_TB) estart[i] = 0;
         int b = 0;
@@ -499,7 +616,8 @@ __global__ __launch_bounds__(DT_TB) void k_dot_task(
             Z v;
             const unsigned long long raw = e_acc[tid];
             __builtin_memcpy(&v, &raw, sizeof(Z));
-            tval[e_q[tid]] = v;
+            if (piece >= 0) dt_global_fold(sr, ANY, &tval[e_q[tid]], v);
+            else tval[e_q[tid]] = v;
             tflag[e_q[tid]] = 1;
         }
         __syncthreads();
@@ -545,6 +663,7 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
     uint8_t *hflag = s.get<uint8_t>(nm);
     gb_memset(hflag, 0, nm);
     uint8_t *tf = s.get<uint8_t>(nm);
+    uint8_t *hg = s.get<uint8_t>(nm);
     int64_t *pos = s.get<int64_t>(nm + 1);
     gb_dispatch_sr(info, [&](auto srf, auto x, auto z) {
         using SRT = decltype(srf);
@@ -568,40 +687,108 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
             if (!(skip & 1))
                 hipLaunchKernelGGL((k_dot_small<SRT, X, Z, SWAP, DT_MID / 64>), dim3(gw), dim3(DT_BLOCK), 0,
                                    gb_stream(), srf, sd, xv, xiso, yv, yiso, (Z *)tval, tflag);
+            // lists longer than the cap run as pieces of cap keys (4- and 8-byte results:
+            // the pieces of an entry fold into its output slot with atomics)
+            const bool pieces = (sizeof(Z) == 4 || sizeof(Z) == 8) && gb_knob("dot_pieces") != 1;
             gb_memset(tf, 0, nm);
-            hipLaunchKernelGGL((k_dt_classify<SWAP>), dim3(gw), dim3(DT_BLOCK), 0, gb_stream(), sd, cap, tf, hflag);
+            if (pieces) gb_memset(hg, 0, nm);
+            hipLaunchKernelGGL((k_dt_classify<SWAP>), dim3(gw), dim3(DT_BLOCK), 0, gb_stream(), sd, cap, tf, hflag,
+                               pieces ? hg : nullptr);
             GB_LAUNCH_CHECK();
+            // tasks over (eG, eYS, eO, eB, eQ) in task order: cut at group changes and windows
+            auto run_tasks = [&](int64_t ne, int32_t *eG, int64_t *eYS, int32_t *eO, int32_t *eB, int64_t *eQ,
+                                 int piece) {
+                gb_scratch ts;
+                int64_t *cum = ts.get<int64_t>(ne + 1);
+                gb_exclusive_scan_i32(eB, DT_OVH, cum, ne);
+                uint8_t *tsf = ts.get<uint8_t>(ne);
+                hipLaunchKernelGGL(k_dt_task_flags, dim3(dt_grid(ne)), dim3(DT_BLOCK), 0, gb_stream(), ne, win, eG,
+                                   cum, tsf);
+                int64_t *tpos = ts.get<int64_t>(ne + 1);
+                gb_exclusive_scan_u8(tsf, tpos, ne);
+                const int64_t nt = gb_read_i64(tpos + ne);
+                int64_t *tstart = ts.get<int64_t>(nt + 1);
+                hipLaunchKernelGGL(k_dt_task_fill, dim3(dt_grid(ne)), dim3(DT_BLOCK), 0, gb_stream(), ne, tsf, tpos,
+                                   tstart);
+                GB_LAUNCH_CHECK();
+                // persistent workgroups: one per CU
+                const unsigned gt = (unsigned)std::min<int64_t>(nt, 1024);
+                if (!(skip & 2))
+                    hipLaunchKernelGGL((k_dot_task<SRT, X, Z, SWAP>), dim3(gt), dim3(DT_TB), 0, gb_stream(), srf,
+                                       info.mon, sd, xv, xiso, yv, yiso, nt, tstart, eG, eYS, eO, eB, eQ, (Z *)tval,
+                                       tflag, (int)gb_knob("dot_dbg"), piece, cap);
+                GB_LAUNCH_CHECK();
+            };
             gb_exclusive_scan_u8(tf, pos, nm);
             const int64_t ne = gb_read_i64(pos + nm);
-            if (ne == 0) return;
-            gb_scratch ts;
-            int32_t *eG = ts.get<int32_t>(ne);
-            int64_t *eYS = ts.get<int64_t>(ne);
-            int32_t *eO = ts.get<int32_t>(ne);
-            int32_t *eB = ts.get<int32_t>(ne);
-            int64_t *eQ = ts.get<int64_t>(ne);
-            hipLaunchKernelGGL((k_dt_compact<SWAP>), dim3(gw), dim3(DT_BLOCK), 0, gb_stream(), sd, cap, tf, pos, eG,
-                               eYS, eO, eB, eQ);
+            if (ne) {
+                gb_scratch es;
+                int32_t *eG = es.get<int32_t>(ne);
+                int64_t *eYS = es.get<int64_t>(ne);
+                int32_t *eO = es.get<int32_t>(ne);
+                int32_t *eB = es.get<int32_t>(ne);
+                int64_t *eQ = es.get<int64_t>(ne);
+                hipLaunchKernelGGL((k_dt_compact<SWAP>), dim3(gw), dim3(DT_BLOCK), 0, gb_stream(), sd, cap, tf, pos,
+                                   eG, eYS, eO, eB, eQ, false, nullptr);
+                GB_LAUNCH_CHECK();
+                run_tasks(ne, eG, eYS, eO, eB, eQ, -1);
+            }
+            if (!pieces) return;
+            gb_exclusive_scan_u8(hg, pos, nm);
+            const int64_t nh = gb_read_i64(pos + nm);
+            if (nh == 0) return;
+            // few huge entries: the per-entry kernel costs less than the piece passes' fixed
+            // work (R-MAT s20: 40k entries per phase, 1.5 ms slower as pieces; s22: 937k,
+            // 15 ms faster); knob dot_pmin overrides
+            int64_t pmin = gb_knob("dot_pmin");
+            if (pmin <= 0) pmin = 131072;
+            if (gb_knob("dot_dbg") & 16) fprintf(stderr, "dot phase %d: %lld huge entries\n", (int)SWAP, (long long)nh);
+            if (nh < pmin) {
+                hipLaunchKernelGGL(k_dt_huge_to_csr, dim3(dt_grid(nm)), dim3(DT_BLOCK), 0, gb_stream(), nm, hg, sd.perm,
+                                   hflag);
+                GB_LAUNCH_CHECK();
+                return;
+            }
+            gb_scratch hs;
+            int32_t *hG = hs.get<int32_t>(nh);
+            int64_t *hYS = hs.get<int64_t>(nh);
+            int32_t *hO = hs.get<int32_t>(nh);
+            int32_t *hB = hs.get<int32_t>(nh);
+            int64_t *hQ = hs.get<int64_t>(nh);
+            unsigned long long *amax = hs.get<unsigned long long>(1);
+            gb_memset(amax, 0, sizeof(unsigned long long));
+            hipLaunchKernelGGL((k_dt_compact<SWAP>), dim3(gw), dim3(DT_BLOCK), 0, gb_stream(), sd, cap, hg, pos, hG,
+                               hYS, hO, hB, hQ, true, amax);
+            Z ident = Z();
+            if (!(std::is_same<SRT, gb_sr_any_pair<Z>>::value || info.mon == GBAMD_MON_ANY))
+                ident = gb_monoid_identity<Z>(info.mon);
+            hipLaunchKernelGGL((k_dt_ident<Z>), dim3(dt_grid(nh)), dim3(DT_BLOCK), 0, gb_stream(), nh, hQ, (Z *)tval,
+                               ident);
             GB_LAUNCH_CHECK();
-            int64_t *cum = ts.get<int64_t>(ne + 1);
-            gb_exclusive_scan_i32(eB, DT_OVH, cum, ne);
-            uint8_t *tsf = ts.get<uint8_t>(ne);
-            hipLaunchKernelGGL(k_dt_task_flags, dim3(dt_grid(ne)), dim3(DT_BLOCK), 0, gb_stream(), ne, win, eG, cum,
-                               tsf);
-            int64_t *tpos = ts.get<int64_t>(ne + 1);
-            gb_exclusive_scan_u8(tsf, tpos, ne);
-            const int64_t nt = gb_read_i64(tpos + ne);
-            int64_t *tstart = ts.get<int64_t>(nt + 1);
-            hipLaunchKernelGGL(k_dt_task_fill, dim3(dt_grid(ne)), dim3(DT_BLOCK), 0, gb_stream(), ne, tsf, tpos,
-                               tstart);
-            GB_LAUNCH_CHECK();
-            // persistent workgroups: one per CU
-            const unsigned gt = (unsigned)std::min<int64_t>(nt, 1024);
-            if (!(skip & 2))
-            hipLaunchKernelGGL((k_dot_task<SRT, X, Z, SWAP>), dim3(gt), dim3(DT_TB), 0, gb_stream(), srf, info.mon,
-                               sd, xv, xiso, yv, yiso, nt, tstart, eG, eYS, eO, eB, eQ, (Z *)tval, tflag,
-                               (int)gb_knob("dot_dbg"));
-            GB_LAUNCH_CHECK();
+            const int64_t amx = gb_read_i64((const int64_t *)amax);
+            const int np = (int)((amx + cap - 1) / cap);
+            uint8_t *pc = hs.get<uint8_t>(nh);
+            int64_t *ppos = hs.get<int64_t>(nh + 1);
+            int64_t *pys = hs.get<int64_t>(nh);
+            int32_t *pb = hs.get<int32_t>(nh);
+            for (int j = 0; j < np; j++) {
+                hipLaunchKernelGGL(k_dt_piece_flags, dim3(dt_grid(nh)), dim3(DT_BLOCK), 0, gb_stream(), sd, nh, j,
+                                   cap, hG, hYS, hB, pc, pys, pb);
+                GB_LAUNCH_CHECK();
+                gb_exclusive_scan_u8(pc, ppos, nh);
+                const int64_t npe = gb_read_i64(ppos + nh);
+                if (npe == 0) continue;
+                gb_scratch ps;
+                int32_t *eG = ps.get<int32_t>(npe);
+                int64_t *eYS = ps.get<int64_t>(npe);
+                int32_t *eO = ps.get<int32_t>(npe);
+                int32_t *eB = ps.get<int32_t>(npe);
+                int64_t *eQ = ps.get<int64_t>(npe);
+                hipLaunchKernelGGL(k_dt_piece_compact, dim3(dt_grid(nh)), dim3(DT_BLOCK), 0, gb_stream(), nh, cap, pc,
+                                   ppos, hG, hO, hQ, pys, pb, eG, eYS, eO, eB, eQ);
+                GB_LAUNCH_CHECK();
+                run_tasks(npe, eG, eYS, eO, eB, eQ, j);
+            }
         };
         phase(std::false_type{});
         phase(std::true_type{});
