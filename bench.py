@@ -589,7 +589,8 @@ def main():
     alg_bytes = len(roots) * (4 * int(ap[-1]) + 8 * (nloc + 1)) + levels_total * 3 * ((n + 7) // 8)
     achieved = alg_bytes / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else None
     traffic = None
-    if os.path.exists(args.traffic_file):
+    # the committed PMC traffic is per launch of the single-GPU kernel (whole matrix): N = 1 only
+    if world == 1 and os.path.exists(args.traffic_file):
         try:
             traffic = json.load(open(args.traffic_file)).get("bytes_per_launch")
         except Exception:
