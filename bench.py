@@ -54,6 +54,7 @@ def parse():
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-secondary", action="store_true", help="skip the config 2 / config 4 lines")
+    p.add_argument("--no-msbfs", action="store_true", help="skip the multi-source (masked mxm) BFS line")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     # rehearsal of the N>1 path on one GPU: all ranks on one device, gloo transport
@@ -128,6 +129,79 @@ def secondary_workloads(lib, torch, stream, O, args):
     for s4 in (20, 22):
         out[f"config4_masked_spgemm_min_plus_int64_s{s4}"] = config4_masked_spgemm(lib, torch, stream, O, args, s4)
     return out
+
+
+def config3_msbfs(lib, torch, stream, O, args, A, n, ap, ai, deg, roots16):
+    """Config 3's workload as a masked GrB_mxm: K level BFSs at once (LAGraph's multi-source
+    form of the reference notebook loop), Q and V K x n:
+        V<Q.V> = d;  Q<!V.S, replace> = Q lor.land A;  until Q.nvals == 0
+    K = 64 roots (the 16 headline roots first), R-MAT s22, timed from a fresh Q to the last
+    nvals.  GTEPS = sum over the K roots of the edges incident to each root's reached set
+    (the headline's convention) / time.  Parity: rows of V vs the oracle's level BFS."""
+    K = 64
+    rng = np.random.default_rng(args.seed + 1)
+    pool = np.setdiff1d(np.flatnonzero(deg > 0), roots16)
+    roots = np.concatenate([roots16, rng.choice(pool, K - len(roots16), replace=False)]).astype(np.uint64)
+    Q, V = ctypes.c_void_p(), ctypes.c_void_p()
+    ok(lib.GrB_Matrix_new(ctypes.byref(Q), lib.GrB_BOOL, K, n), "Q")
+    ok(lib.GrB_Matrix_new(ctypes.byref(V), lib.GrB_INT32, K, n), "V")
+    qi = np.arange(K, dtype=np.uint64)
+    nv = ctypes.c_uint64()
+    sr, desc, grb_all = lib.GrB_LOR_LAND_SEMIRING_BOOL, lib.GrB_DESC_RSC, lib.GrB_ALL
+
+    def batch():
+        ok(lib.GrB_Matrix_clear(Q), "clear Q")
+        ok(lib.GrB_Matrix_clear(V), "clear V")
+        # iso build (one scalar for every entry), as from_coo(rows, cols, True) issues it
+        ok(lib.GxB_Matrix_build_Scalar_BOOL(Q, ctypes.c_void_p(qi.ctypes.data), ctypes.c_void_p(roots.ctypes.data),
+                                            True, K), "build Q")
+        d = 0
+        while True:
+            d += 1
+            ok(lib.GrB_Matrix_assign_INT32(V, Q, None, d, grb_all, K, grb_all, n, None), "V<Q> = d")
+            ok(lib.GrB_mxm(Q, V, None, sr, Q, A, desc), "Q<!V.S> = Q lor.land A")
+            ok(lib.GrB_Matrix_nvals(ctypes.byref(nv), Q), "nvals")
+            if nv.value == 0:
+                return d
+
+    levels = batch()
+    # parity + edge counts (untimed): extract V
+    ok(lib.GrB_Matrix_nvals(ctypes.byref(nv), V), "nvals V")
+    m = nv.value
+    vi = np.empty(m, np.uint64)
+    vj = np.empty(m, np.uint64)
+    vx = np.empty(m, np.int32)
+    cnt = ctypes.c_uint64(m)
+    ok(lib.GrB_Matrix_extractTuples_INT32(ctypes.c_void_p(vi.ctypes.data), ctypes.c_void_p(vj.ctypes.data),
+                                          ctypes.c_void_p(vx.ctypes.data), ctypes.byref(cnt), V), "extract V")
+    vi, vj = vi.astype(np.int64), vj.astype(np.int64)
+    edges = int(np.bincount(vi, weights=deg[vj], minlength=K).sum())
+    G = O.Csr(n, n, "BOOL", ap, ai, np.ones(ai.size, np.bool_))
+    parity = True
+    for r in (0, K - 1):
+        lev, _, _ = O.bfs_levels(G, int(roots[r]))
+        got = np.zeros(n, np.int32)
+        sel = vi == r
+        got[vj[sel]] = vx[sel]
+        parity = parity and bool(np.array_equal(got, lev))
+    if not parity:
+        raise SystemExit("multi-source BFS parity failure vs oracle")
+    del vi, vj, vx
+    for _ in range(2):
+        batch()
+    torch.cuda.synchronize()
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        batch()
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / reps
+    ok(lib.GrB_Matrix_free(ctypes.byref(Q)), "free Q")
+    ok(lib.GrB_Matrix_free(ctypes.byref(V)), "free V")
+    return {"workload": f"multi-source level BFS, {K} roots at once: V<Q.V> = d; Q<!V.S,replace> = Q lor.land A "
+                        f"(GrB_Matrix_assign + masked GrB_mxm, Q/V {K} x n), R-MAT s{args.scale}",
+            "roots": K, "levels": levels, "ms_per_batch": el * 1e3, "gteps": edges / el / 1e9,
+            "edges": edges, "parity_vs_oracle_2_roots": parity}
 
 
 def config2_spmv(lib, torch, stream, args, scale, ef):
@@ -610,8 +684,10 @@ def main():
         del xs, ys
 
     secondary = {}
+    if rank == 0 and world == 1 and not args.no_msbfs:
+        secondary["config3_msbfs_64_roots"] = config3_msbfs(lib, torch, stream, O, args, A, n, ap, ai, deg, roots)
     if rank == 0 and world == 1 and not args.no_secondary:
-        secondary = secondary_workloads(lib, torch, stream, O, args)
+        secondary.update(secondary_workloads(lib, torch, stream, O, args))
     if not args.no_spgemm:
         secondary["config5_spgemm_plus_times_fp64"] = config5_spgemm(lib, torch, stream, dist, world, rank, args)
 

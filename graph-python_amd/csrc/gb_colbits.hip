@@ -1,0 +1,594 @@
+// gb_colbits.hip -- batched frontiers: GrB_mxm with a left operand of at most 64
+// rows over a boolean (LOR / ANY) semiring, and the masked scalar assign that
+// stamps levels, on a column-word bitmap format.
+//
+// Why: a multi-source BFS in GraphBLAS (k roots at once, LAGraph style) is
+//     V<Q.V> = d;  Q<!V.S, replace> = Q lor.land A      (Q, V: k x n)
+// i.e. the north-star's masked GrB_mxm (reference core/matrix.py:2241, dispatched
+// by core/base.py:483) with Q and V as the k-row operands.  Held as CSR, every
+// level would rewrite V's whole row structure (k x n entries at the end) and Q's;
+// SuiteSparse switches such matrices to its bitmap format.  Here a matrix of
+// k <= 64 rows switches to column words: cw[j] holds the k presence bits of
+// column j (bit r = entry (r, j)), values column-major (cw_vals[j * k + r]).
+// Then one level is one pass over the graph for all k sources:
+//   pull (rows of B^T = in-edges of output column j):  out[j] = OR_i F[i] & need(j),
+//        need(j) = the mask's complement in column j; a lane walks its column's
+//        first CAP edges alone (4 gathers in flight), stops as soon as every needed
+//        bit is found, and hands longer columns to the whole wave (256 edges a
+//        step, wave OR-reduction, same early exit);
+//   push (rows of B = out-edges of frontier column i):  atomicOr(out[j], F[i] & need(j))
+//        with a pre-check, newly set bits counted from the atomic's old value.
+// Direction is chosen on the device (Beamer): push iff the frontier's out-edges x
+// alpha < nnz(B); each level's kernel leaves the next level's edge count
+// (cw_stat[1]) and the count (cw_stat[0], published to the host mailbox).
+// Result values: a boolean LOR/ANY fold of iso operands is iso, its value
+// mult(a, b) computed on the device, so structure is all the kernel produces.
+// Bytes per level (pull): 4 B per scanned edge + 8 B gather per scanned edge
+// (F is n x 8 B = 32 MB at s22: MALL-resident) + 8 B mask + 8 B output per column.
+//
+// Every other API entry point sees CSR: gb_obj_check converts back (gb_cw_to_csr:
+// per-column popcounts, scan, CSC fill, transpose).
+#include <algorithm>
+
+#include "gb_dispatch.cuh"
+#include "gb_internal.h"
+
+namespace {
+
+constexpr int CB_BLOCK = 256;
+constexpr int CB_CAP = 32;  // edges a lane walks alone before the wave takes its column over
+
+GB_DEV uint64_t cb_shfl(uint64_t v, int src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+GB_DEV int64_t cb_shfl_i64(int64_t v, int src) { return (int64_t)cb_shfl((uint64_t)v, src); }
+GB_DEV uint64_t cb_wave_or(uint64_t v) {
+    for (int off = 32; off > 0; off >>= 1) v |= cb_shfl(v, (int)(threadIdx.x & 63) ^ off);
+    return v;
+}
+GB_DEV bool cb_nonzero(const void *p, int size) {
+    switch (size) {
+        case 1: return *(const uint8_t *)p != 0;
+        case 2: return *(const uint16_t *)p != 0;
+        case 4: return *(const uint32_t *)p != 0;
+        default: return *(const uint64_t *)p != 0;
+    }
+}
+GB_DEV void cb_copy(void *dst, const void *src, int size) {
+    switch (size) {
+        case 1: *(uint8_t *)dst = *(const uint8_t *)src; break;
+        case 2: *(uint16_t *)dst = *(const uint16_t *)src; break;
+        case 4: *(uint32_t *)dst = *(const uint32_t *)src; break;
+        default: *(uint64_t *)dst = *(const uint64_t *)src; break;
+    }
+}
+GB_DEV void cb_publish(gb_host_slot *pub, long long seq, long long value) {
+    if (!pub) return;
+    __hip_atomic_store(&pub->value, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+    __hip_atomic_store(&pub->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+struct cb_step_args {
+    int64_t nout, nin, nnz;
+    const uint64_t *F;                      // input column words [nin]
+    const int64_t *prp;                     // pull CSR: rows = output columns, entries = input columns
+    const int32_t *pci;
+    const int64_t *srp;                     // push CSR: rows = input columns (nullptr: pull only)
+    const int32_t *sci;
+    const uint64_t *M;                      // mask words [nout] (nullptr: no mask)
+    const void *m_iso;                      // value mask of an iso matrix: its value (nullptr: structure)
+    int m_iso_size;
+    bool comp;
+    uint64_t full;                          // the k row bits
+    uint64_t *out;                          // [nout], zeroed
+    const int64_t *stat_in;                 // F's [count, out-edges]
+    int64_t alpha;
+    int dir;                                // 0 auto, 1 pull, 2 push
+    int64_t *stat_out;
+    unsigned long long *gst, *gst2;
+    gb_host_slot *pub;
+    long long seq;
+    const uint8_t *a_val, *b_val;           // iso values of the operands (nullptr: not iso)
+    int mul;
+    uint8_t *out_val;
+};
+
+GB_DEV uint64_t cb_need(const cb_step_args &a, int64_t j, bool m_on) {
+    if (!a.M) return a.full;
+    const uint64_t m = m_on ? a.M[j] : 0ULL;
+    return a.comp ? (~m & a.full) : (m & a.full);
+}
+
+GB_DEV bool cb_mult_value(int mul, bool x, bool y) {
+    switch (mul) {
+        case GBAMD_OP_FIRST: return x;
+        case GBAMD_OP_SECOND: return y;
+        case GBAMD_OP_PAIR: return true;
+        case GBAMD_OP_LOR:
+        case GBAMD_OP_MAX: return x || y;
+        default: return x && y;  // LAND, TIMES, MIN
+    }
+}
+
+// One level of C<M> = F lor.land B (or any.pair ...): pull or push, chosen from
+// stat_in on the device.  All blocks call the grid sums once.
+__global__ __launch_bounds__(CB_BLOCK) void k_cw_step(cb_step_args a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const bool m_on = !a.m_iso || cb_nonzero(a.m_iso, a.m_iso_size);
+    const bool push = a.srp && (a.dir == 2 || (a.dir == 0 && a.stat_in[1] * a.alpha < a.nnz));
+    long long cnt = 0, hint = 0;
+    if (!push) {
+        for (int64_t base = wave * 64; base < a.nout; base += nwaves * 64) {
+            const int64_t j = base + lane;
+            uint64_t need = 0, acc = 0;
+            int64_t p = 0, e = 0;
+            if (j < a.nout) {
+                need = cb_need(a, j, m_on);
+                if (need) {
+                    p = a.prp[j];
+                    e = a.prp[j + 1];
+                }
+            }
+            const int64_t lim = e < p + CB_CAP ? e : p + CB_CAP;
+            while (p < lim) {
+                uint64_t f = a.F[a.pci[p]];
+                if (p + 1 < lim) f |= a.F[a.pci[p + 1]];
+                if (p + 2 < lim) f |= a.F[a.pci[p + 2]];
+                if (p + 3 < lim) f |= a.F[a.pci[p + 3]];
+                acc |= f;
+                p += 4;
+                if ((acc & need) == need) break;
+            }
+            const bool more = (acc & need) != need && p < e;
+            uint64_t longs = __ballot(more);
+            while (longs) {
+                const int L = __ffsll((unsigned long long)longs) - 1;
+                longs &= longs - 1;
+                const int64_t pL = cb_shfl_i64(p, L), eL = cb_shfl_i64(e, L);
+                const uint64_t nL = cb_shfl(need, L);
+                uint64_t aL = cb_shfl(acc, L);
+                for (int64_t qb = pL; qb < eL; qb += 256) {
+                    uint64_t f = 0;
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const int64_t q = qb + lane + 64 * u;
+                        if (q < eL) f |= a.F[a.pci[q]];
+                    }
+                    aL |= cb_wave_or(f);
+                    if ((aL & nL) == nL) break;
+                }
+                if (lane == L) acc = aL;
+            }
+            if (j < a.nout) {
+                const uint64_t w = acc & need;
+                a.out[j] = w;
+                cnt += __popcll(w);
+                if (w && a.srp && j < a.nin) hint += a.srp[j + 1] - a.srp[j];
+            }
+        }
+    } else {
+        auto push_one = [&](int64_t j, uint64_t f) {
+            const uint64_t nb = f & cb_need(a, j, m_on);
+            if (!nb) return;
+            const uint64_t cur = __hip_atomic_load(&a.out[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((cur & nb) == nb) return;
+            const uint64_t old = atomicOr((unsigned long long *)&a.out[j], (unsigned long long)nb);
+            const uint64_t add = nb & ~old;
+            cnt += __popcll(add);
+            if (old == 0 && add && j < a.nin) hint += a.srp[j + 1] - a.srp[j];
+        };
+        for (int64_t base = wave * 64; base < a.nin; base += nwaves * 64) {
+            const int64_t i = base + lane;
+            const uint64_t f = i < a.nin ? a.F[i] : 0ULL;
+            int64_t p = 0, e = 0;
+            if (f) {
+                p = a.srp[i];
+                e = a.srp[i + 1];
+            }
+            const int64_t lim = e < p + CB_CAP ? e : p + CB_CAP;
+            for (; p < lim; p++) push_one(a.sci[p], f);
+            uint64_t longs = __ballot(p < e);
+            while (longs) {
+                const int L = __ffsll((unsigned long long)longs) - 1;
+                longs &= longs - 1;
+                const int64_t pL = cb_shfl_i64(p, L), eL = cb_shfl_i64(e, L);
+                const uint64_t fL = cb_shfl(f, L);
+                for (int64_t q = pL + lane; q < eL; q += 64) push_one(a.sci[q], fL);
+            }
+        }
+    }
+    long long tot;
+    if (gb_grid_sum(cnt, a.gst, &tot)) {
+        a.stat_out[0] = tot;
+        cb_publish(a.pub, a.seq, tot);
+    }
+    if (gb_grid_sum(hint, a.gst2, &tot)) a.stat_out[1] = tot;
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        *a.out_val = cb_mult_value(a.mul, a.a_val ? *a.a_val != 0 : true, a.b_val ? *a.b_val != 0 : true);
+}
+
+// stat[1] = out-edges (rows of srp) of the non-empty columns of F
+__global__ __launch_bounds__(CB_BLOCK) void k_cw_hint(const uint64_t *__restrict__ F, int64_t n,
+                                                       const int64_t *__restrict__ srp, int64_t *__restrict__ stat,
+                                                       unsigned long long *gst) {
+    long long h = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        if (F[i]) h += srp[i + 1] - srp[i];
+    long long tot;
+    if (gb_grid_sum(h, gst, &tot)) stat[1] = tot;
+}
+
+// CSR (k rows) -> column words; stat = [nvals, out-edges of the entries' columns in srp]
+__global__ __launch_bounds__(CB_BLOCK) void k_csr_to_cw(int k, int64_t nvals, const int64_t *__restrict__ rowptr,
+                                                         const int32_t *__restrict__ colidx, const uint8_t *vals,
+                                                         int vsize, uint64_t *__restrict__ cw, uint8_t *cwv,
+                                                         const int64_t *__restrict__ srp, int64_t nsrp,
+                                                         int64_t *__restrict__ stat, unsigned long long *gst) {
+    long long h = 0;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nvals;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        int lo = 0, hi = k;  // row r: rowptr[r] <= e < rowptr[r + 1]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (rowptr[mid] <= e) lo = mid;
+            else hi = mid;
+        }
+        const int64_t j = colidx[e];
+        atomicOr((unsigned long long *)&cw[j], 1ULL << lo);
+        if (cwv) cb_copy(cwv + (j * k + lo) * vsize, vals + e * vsize, vsize);
+        if (srp && j < nsrp) h += srp[j + 1] - srp[j];
+    }
+    long long tot;
+    if (gb_grid_sum(h, gst, &tot)) {
+        stat[0] = nvals;
+        stat[1] = tot;
+    }
+}
+
+__global__ void k_cw_pop(const uint64_t *__restrict__ cw, int64_t n, int64_t *__restrict__ pop) {
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x)
+        pop[j] = __popcll(cw[j]);
+}
+
+// CSC of a column-word matrix: column j's rows in ascending order (+ values)
+__global__ void k_cw_fill(const uint64_t *__restrict__ cw, int64_t n, int k, const int64_t *__restrict__ cptr,
+                          int32_t *__restrict__ ridx, const uint8_t *cwv, uint8_t *tv, int vsize) {
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t w = cw[j];
+        int64_t o = cptr[j];
+        while (w) {
+            const int r = __ffsll((unsigned long long)w) - 1;
+            w &= w - 1;
+            ridx[o] = r;
+            if (tv) cb_copy(tv + o * vsize, cwv + (j * k + r) * vsize, vsize);
+            o++;
+        }
+    }
+}
+
+// C<M> = x (all indices, no accum): bits OR'ed in, x stored at the mask's entries,
+// count delta added to stat[0]
+__global__ __launch_bounds__(CB_BLOCK) void k_cw_assign(int64_t n, int k, const uint64_t *__restrict__ M,
+                                                         const void *m_iso, int m_iso_size, const uint8_t *m_vals,
+                                                         int m_vsize, uint64_t *__restrict__ C, uint8_t *cv,
+                                                         unsigned long long x, int vsize, int64_t *stat,
+                                                         unsigned long long *gst) {
+    const bool m_on = !m_iso || cb_nonzero(m_iso, m_iso_size);
+    long long delta = 0;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t m = m_on ? M[j] : 0ULL;
+        if (m && m_vals) {  // value mask: keep the bits whose value is nonzero
+            uint64_t t = m, keep = 0;
+            while (t) {
+                const int r = __ffsll((unsigned long long)t) - 1;
+                t &= t - 1;
+                if (cb_nonzero(m_vals + (j * k + r) * m_vsize, m_vsize)) keep |= 1ULL << r;
+            }
+            m = keep;
+        }
+        if (!m) continue;
+        const uint64_t old = C[j];
+        C[j] = old | m;
+        delta += __popcll(m & ~old);
+        uint64_t t = m;
+        while (t) {
+            const int r = __ffsll((unsigned long long)t) - 1;
+            t &= t - 1;
+            cb_copy(cv + (j * k + r) * vsize, &x, vsize);
+        }
+    }
+    gb_grid_add(delta, (unsigned long long *)stat, gst);
+}
+
+// dense fill of an iso value (expanding an iso column-word matrix)
+__global__ void k_cw_fill_iso(uint8_t *v, int64_t count, const uint8_t *one, int vsize) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < count; e += (int64_t)gridDim.x * blockDim.x)
+        cb_copy(v + e * vsize, one, vsize);
+}
+
+unsigned cb_grid(int64_t items, unsigned cap) {
+    int64_t g = (items + CB_BLOCK - 1) / CB_BLOCK;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+
+unsigned long long *grid_state(int which) {
+    unsigned long long *st = gb_device_state();
+    return which == 0 ? st : st + GB_GRID2_OFFSET;
+}
+
+// A (CSR, 1 <= k <= 64 rows) -> column words in place.  srp (optional): push rows
+// keyed by hint_key for the out-edge hint.
+void to_cw(GB_Obj *A, const int64_t *srp, int64_t nsrp, const void *hint_key) {
+    const int k = (int)A->nrows;
+    const int64_t n = A->ncols, nv = A->nvals;
+    const int vs = (int)A->type->size;
+    uint64_t *cw = gb_malloc_n<uint64_t>(n > 0 ? n : 1);
+    gb_memset(cw, 0, (n > 0 ? n : 1) * sizeof(uint64_t));
+    int64_t *stat = gb_malloc_n<int64_t>(4);
+    gb_memset(stat, 0, 4 * sizeof(int64_t));
+    const bool iso = A->iso && nv > 0;
+    void *cwv;
+    if (iso) {
+        cwv = gb_malloc(vs);
+        gb_copy_d2d(cwv, A->vals, vs);
+    } else {
+        cwv = gb_malloc((size_t)vs * (size_t)k * (size_t)(n > 0 ? n : 1));
+    }
+    if (nv > 0) {
+        hipLaunchKernelGGL(k_csr_to_cw, dim3(cb_grid(nv, 2048)), dim3(CB_BLOCK), 0, gb_stream(), k, nv, A->rowptr,
+                           A->colidx, (const uint8_t *)A->vals, vs, cw, iso ? nullptr : (uint8_t *)cwv, srp, nsrp,
+                           stat, grid_state(0));
+        GB_LAUNCH_CHECK();
+    }
+    gb_drop_transpose(A);
+    gb_free(A->rowptr);
+    gb_free(A->colidx);
+    gb_free(A->vals);
+    A->rowptr = nullptr;
+    A->colidx = nullptr;
+    A->vals = nullptr;
+    A->cw = cw;
+    A->cw_vals = cwv;
+    A->cw_stat = stat;
+    A->iso = iso;
+    A->nvals = nv;
+    A->nvals_valid = true;
+    A->pub_seq = 0;
+    A->hint_valid = srp != nullptr;  // stat[1]: the kernel's sum (or 0 when empty)
+    A->hint_key = hint_key;
+}
+
+// make a column-word matrix's values per-entry (C of an assign)
+void cw_expand(GB_Obj *A) {
+    if (!A->iso) return;
+    const int vs = (int)A->type->size;
+    const int64_t count = A->nrows * A->ncols;
+    uint8_t *v = (uint8_t *)gb_malloc((size_t)vs * (size_t)(count > 0 ? count : 1));
+    if (count > 0) {
+        hipLaunchKernelGGL(k_cw_fill_iso, dim3(cb_grid(count, 4096)), dim3(CB_BLOCK), 0, gb_stream(), v, count,
+                           (const uint8_t *)A->cw_vals, vs);
+        GB_LAUNCH_CHECK();
+    }
+    gb_free(A->cw_vals);
+    A->cw_vals = v;
+    A->iso = false;
+}
+
+bool small_rows(const GB_Obj *A) { return A->kind == GB_KIND_MATRIX && A->nrows >= 1 && A->nrows <= 64; }
+
+}  // namespace
+
+// ================================================================== storage
+void gb_cw_release(GB_Obj *A) {
+    if (!A->cw) return;
+    gb_free(A->cw);
+    gb_free(A->cw_vals);
+    gb_free(A->cw_stat);
+    A->cw = nullptr;
+    A->cw_vals = nullptr;
+    A->cw_stat = nullptr;
+    A->pub_seq = 0;
+    A->hint_valid = false;
+}
+
+void gb_cw_to_csr(GB_Obj *A) {
+    if (!A->cw) return;
+    const int k = (int)A->nrows;
+    const int64_t n = A->ncols;
+    const int vs = (int)A->type->size;
+    const int64_t nv = gb_nvals(A);
+    const bool iso = A->iso && nv > 0;
+    int64_t *rp = nullptr;
+    int32_t *ci = nullptr;
+    void *vv = nullptr;
+    if (nv == 0) {
+        rp = gb_malloc_n<int64_t>(k + 1);
+        gb_memset(rp, 0, (k + 1) * sizeof(int64_t));
+    } else {
+        gb_scratch s;
+        int64_t *pop = s.get<int64_t>(n);
+        int64_t *cptr = s.get<int64_t>(n + 1);
+        int32_t *ridx = s.get<int32_t>(nv);
+        uint8_t *tv = iso ? nullptr : s.get<uint8_t>((size_t)nv * vs);
+        hipLaunchKernelGGL(k_cw_pop, dim3(cb_grid(n, 4096)), dim3(CB_BLOCK), 0, gb_stream(), A->cw, n, pop);
+        GB_LAUNCH_CHECK();
+        gb_exclusive_scan_i64(pop, cptr, n);
+        hipLaunchKernelGGL(k_cw_fill, dim3(cb_grid(n, 4096)), dim3(CB_BLOCK), 0, gb_stream(), A->cw, n, k, cptr, ridx,
+                           (const uint8_t *)A->cw_vals, tv, vs);
+        GB_LAUNCH_CHECK();
+        // (n x k) CSR of A^T -> CSR of A
+        gb_transpose_csr(n, k, nv, cptr, ridx, iso ? A->cw_vals : (const void *)tv, vs, iso, &rp, &ci, &vv);
+    }
+    gb_cw_release(A);
+    A->rowptr = rp;
+    A->colidx = ci;
+    A->vals = vv;
+    A->nvals = nv;
+    A->iso = iso;
+    A->nvals_valid = true;
+}
+
+// ================================================================== C<M> = A (+).(x) B, A of <= 64 rows
+bool gb_colbits_mxm(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, GrB_Semiring sr, GB_Obj *A, GB_Obj *B,
+                    const gb_desc &d) {
+    const int64_t knob = gb_knob("colbits");  // 0 auto, 1 always when legal, 2 never
+    if (knob == 2 || accum || !sr || sr->magic != GB_MAGIC) return false;
+    if (!small_rows(A) || !small_rows(C) || B->kind != GB_KIND_MATRIX || d.tran0) return false;
+    if (B->cw) return false;  // B is the graph; a column-word B takes the general path (converted)
+    const int mon = sr->add->mcode, mul = sr->mul->opcode;
+    if (sr->add->type->code != GBAMD_T_BOOL || (mon != GBAMD_MON_LOR && mon != GBAMD_MON_ANY)) return false;
+    if (!sr->mul->xtype || sr->mul->xtype->code != GBAMD_T_BOOL || sr->mul->ztype->code != GBAMD_T_BOOL) return false;
+    if (A->type->code != GBAMD_T_BOOL || B->type->code != GBAMD_T_BOOL || C->type->code != GBAMD_T_BOOL) return false;
+    const bool uses_a = mul != GBAMD_OP_SECOND && mul != GBAMD_OP_PAIR;
+    const bool uses_b = mul != GBAMD_OP_FIRST && mul != GBAMD_OP_PAIR;
+    switch (mul) {
+        case GBAMD_OP_FIRST: case GBAMD_OP_SECOND: case GBAMD_OP_PAIR: case GBAMD_OP_LAND:
+        case GBAMD_OP_LOR: case GBAMD_OP_TIMES: case GBAMD_OP_MIN: case GBAMD_OP_MAX: break;
+        default: return false;
+    }
+    const int64_t k = A->nrows;
+    const int64_t inner = A->ncols, br = d.tran1 ? B->ncols : B->nrows, bc = d.tran1 ? B->nrows : B->ncols;
+    if (inner != br || C->nrows != k || C->ncols != bc) return false;  // the general path reports it
+    // result values: every product's value is mult(a, b) of the iso operand values
+    if ((uses_a && !(A->iso || (!A->cw && A->nvals == 0))) || (uses_b && !(B->iso || B->nvals == 0))) return false;
+    if (M) {
+        if (!small_rows(M) || M->nrows != k || M->ncols != bc) return false;
+        if (!d.structure && !M->iso && !(M->cw == nullptr && M->nvals == 0)) return false;
+        // C<M> without replace keeps C's entries outside the mask: only when C is empty
+        if (!d.replace && (C->cw || C->nvals != 0)) return false;
+        if (M == B) return false;  // converting M would free the CSR the kernel reads
+    }
+    if (A == B) return false;
+    if (knob == 0 && !A->cw && inner < 4096) return false;  // small problems keep the CSR kernels
+
+    // operand views: pull rows = output columns (B^T), push rows = inner index (B)
+    gb_csr_view pv, sv;
+    if (d.tran1) {
+        gb_get_csr(pv, B);
+        gb_get_csc(sv, B);
+    } else {
+        gb_get_csc(pv, B);
+        gb_get_csr(sv, B);
+    }
+    const bool square = bc == inner;
+    const int64_t dir = gb_knob("colbits_direction");  // 0 auto, 1 pull, 2 push
+    if (!A->cw) to_cw(A, sv.rowptr, inner, sv.rowptr);
+    if (M && !M->cw) to_cw(M, nullptr, 0, nullptr);
+    if (!A->hint_valid || A->hint_key != (const void *)sv.rowptr) {
+        hipLaunchKernelGGL(k_cw_hint, dim3(cb_grid(inner, 1024)), dim3(CB_BLOCK), 0, gb_stream(), A->cw, inner,
+                           sv.rowptr, A->cw_stat, grid_state(0));
+        GB_LAUNCH_CHECK();
+        A->hint_valid = true;
+        A->hint_key = sv.rowptr;
+    }
+    uint64_t *out = gb_malloc_n<uint64_t>(bc > 0 ? bc : 1);
+    int64_t *stat = gb_malloc_n<int64_t>(4);
+    uint8_t *oval = (uint8_t *)gb_malloc(1);
+    if (dir != 1) GB_HIP(hipMemsetAsync(out, 0, (bc > 0 ? bc : 1) * sizeof(uint64_t), gb_stream()));
+    if (!C->pub) C->pub = gb_host_slot_alloc();
+    const uint64_t seq = gb_next_pub_seq();
+
+    cb_step_args a{};
+    a.nout = bc;
+    a.nin = inner;
+    a.nnz = sv.nvals;
+    a.F = A->cw;
+    a.prp = pv.rowptr;
+    a.pci = pv.colidx;
+    a.srp = dir == 1 ? nullptr : sv.rowptr;
+    a.sci = dir == 1 ? nullptr : sv.colidx;
+    a.M = M ? M->cw : nullptr;
+    a.m_iso = (M && !d.structure && M->iso) ? M->cw_vals : nullptr;
+    a.m_iso_size = M ? (int)M->type->size : 1;
+    a.comp = d.comp;
+    a.full = k == 64 ? ~0ULL : ((1ULL << k) - 1);
+    a.out = out;
+    a.stat_in = A->cw_stat;
+    int64_t alpha = gb_knob("colbits_alpha");
+    a.alpha = alpha > 0 ? alpha : 8;
+    a.dir = (int)dir;
+    a.stat_out = stat;
+    a.gst = grid_state(0);
+    a.gst2 = grid_state(1);
+    a.pub = gb_host_slot_device(C->pub);
+    a.seq = (long long)seq;
+    a.a_val = (uses_a && A->iso) ? (const uint8_t *)A->cw_vals : nullptr;
+    a.b_val = (uses_b && B->iso) ? (const uint8_t *)B->vals : nullptr;
+    a.mul = mul;
+    a.out_val = oval;
+    // enough waves to cover the output in a few chunks each; every block joins the grid sums
+    hipLaunchKernelGGL(k_cw_step, dim3(cb_grid((bc > inner ? bc : inner), 2048)), dim3(CB_BLOCK), 0, gb_stream(), a);
+    GB_LAUNCH_CHECK();
+
+    // install into C (stream-ordered frees: the kernel has read A/M before they go)
+    if (C->kind == GB_KIND_MATRIX && !C->cw) {
+        gb_drop_transpose(C);
+        gb_free(C->rowptr);
+        gb_free(C->colidx);
+        gb_free(C->vals);
+        C->rowptr = nullptr;
+        C->colidx = nullptr;
+        C->vals = nullptr;
+    } else {
+        gb_free(C->cw);
+        gb_free(C->cw_vals);
+        gb_free(C->cw_stat);
+    }
+    C->cw = out;
+    C->cw_vals = oval;
+    C->cw_stat = stat;
+    C->iso = true;
+    C->nvals_valid = false;
+    C->hint_valid = square && a.srp != nullptr;
+    C->hint_key = sv.rowptr;
+    C->pub_seq = seq;
+    C->pub_epoch = gb_epoch();
+    return true;
+}
+
+// ================================================================== C<M> = x, C of <= 64 rows
+bool gb_colbits_assign_scalar(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, const void *x, int xcode,
+                              const GrB_Index *I, const GrB_Index *J, const gb_desc &d) {
+    const int64_t knob = gb_knob("colbits");
+    if (knob == 2 || accum || I != GrB_ALL || J != GrB_ALL || !M || d.comp || d.replace) return false;
+    if (!small_rows(C) || !small_rows(M) || M->nrows != C->nrows || M->ncols != C->ncols) return false;
+    if (C->type->code >= GBAMD_T_COUNT || M->type->code >= GBAMD_T_COUNT) return false;
+    // auto: when either side already is column words, or the matrix is wide (the general
+    // path materialises every index pair of a whole-matrix assign)
+    if (knob == 0 && !C->cw && !M->cw && C->ncols < 4096) return false;
+    const int64_t k = C->nrows, n = C->ncols;
+    const int vs = (int)C->type->size;
+    if ((double)k * (double)n * vs > 64e9) return false;
+    unsigned long long xv = 0;
+    gb_with_type(C->type->code, [&](auto z) {
+        using D = decltype(z);
+        gb_with_type(xcode, [&](auto y) {
+            using S = decltype(y);
+            S s;
+            memcpy(&s, x, sizeof(S));
+            D dv = gb_cast<D, S>(s);
+            memcpy(&xv, &dv, sizeof(D));
+        });
+    });
+    if (!M->cw) to_cw(M, nullptr, 0, nullptr);
+    if (!C->cw) to_cw(C, nullptr, 0, nullptr);
+    cw_expand(C);
+    const bool value_mask = !d.structure;
+    const void *m_iso = (value_mask && M->iso) ? M->cw_vals : nullptr;
+    const uint8_t *m_vals = (value_mask && !M->iso) ? (const uint8_t *)M->cw_vals : nullptr;
+    hipLaunchKernelGGL(k_cw_assign, dim3(cb_grid(n, 2048)), dim3(CB_BLOCK), 0, gb_stream(), n, (int)k, M->cw, m_iso,
+                       (int)M->type->size, m_vals, (int)M->type->size, C->cw, (uint8_t *)C->cw_vals, xv, vs,
+                       C->cw_stat, grid_state(0));
+    GB_LAUNCH_CHECK();
+    C->nvals_valid = false;
+    C->pub_seq = 0;
+    C->hint_valid = false;
+    return true;
+}

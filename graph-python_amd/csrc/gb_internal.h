@@ -120,6 +120,16 @@ struct GB_Matrix_opaque {
     bool hint_valid;
     const void *hint_key;
     std::string err;
+    // ---- column-word bitmap (kind == MATRIX, 1 <= nrows <= 64): the batched-frontier
+    // format of gb_colbits.hip.  cw != nullptr: the matrix is held as cw[ncols]
+    // presence words (bit r of cw[j] = entry (r, j)) and values cw_vals[j * nrows + r]
+    // (or [1] when iso); rowptr/colidx/vals are empty, the count lives in cw_stat[0]
+    // (+ the pub mailbox, like a vector's), cw_stat[1] holds the edge hint keyed by
+    // hint_key.  Every API entry point outside gb_colbits.hip sees CSR: gb_obj_check
+    // converts back (gb_cw_to_csr).
+    uint64_t *cw;
+    void *cw_vals;
+    int64_t *cw_stat;
     // set when a deferred operation on this object failed after its call returned
     // (GrB_INVALID_OBJECT from then on, C API 2.0 nonblocking execution errors)
     GrB_Info invalid = GrB_SUCCESS;
@@ -236,7 +246,11 @@ struct gb_scratch {
 };
 
 // ------------------------------------------------------------------ objects
-GB_Obj *gb_obj_check(const void *p, bool allow_null = false);
+GB_Obj *gb_obj_check(const void *p, bool allow_null = false);      // CSR for matrices
+GB_Obj *gb_obj_check_raw(const void *p, bool allow_null = false);  // any internal format
+// column-word bitmap matrices (gb_colbits.hip)
+void gb_cw_to_csr(GB_Obj *A);    // back to CSR (device work; reads the count)
+void gb_cw_release(GB_Obj *A);   // drop the column-word storage without converting
 GB_Obj *gb_new_object(int kind, GrB_Type type, int64_t nrows, int64_t ncols);
 void gb_obj_free_storage(GB_Obj *A);
 void gb_drop_transpose(GB_Obj *A);
@@ -334,6 +348,13 @@ struct gb_desc {
     bool replace = false, comp = false, structure = false, tran0 = false, tran1 = false;
 };
 gb_desc gb_read_desc(const GrB_Descriptor d);
+// batched-frontier fast paths (gb_colbits.hip): C<M> = A lor.land B with A of at most 64
+// rows, and C<M> = x over all indices; false when the call is not of that shape (the
+// caller then runs the general path on CSR operands)
+bool gb_colbits_mxm(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, GrB_Semiring sr, GB_Obj *A, GB_Obj *B,
+                    const gb_desc &d);
+bool gb_colbits_assign_scalar(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, const void *x, int xcode,
+                              const GrB_Index *I, const GrB_Index *J, const gb_desc &d);
 
 // Effective mask: bitmap of positions where the mask is true (value masks cast
 // to bool), for vector outputs; CSR (structure only) for matrix outputs.

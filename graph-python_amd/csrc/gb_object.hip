@@ -42,6 +42,12 @@ static void with_type(int code, F &&f) {
 
 // ================================================================== object basics
 GB_Obj *gb_obj_check(const void *p, bool allow_null) {
+    GB_Obj *A = gb_obj_check_raw(p, allow_null);
+    if (A && A->cw) gb_cw_to_csr(A);
+    return A;
+}
+
+GB_Obj *gb_obj_check_raw(const void *p, bool allow_null) {
     if (!p) {
         if (allow_null) return nullptr;
         gb_throw(GrB_NULL_POINTER, "required object is NULL");
@@ -140,6 +146,7 @@ void gb_drop_transpose(GB_Obj *A) {
 }
 
 void gb_obj_free_storage(GB_Obj *A) {
+    gb_cw_release(A);
     gb_drop_transpose(A);
     gb_free(A->rowptr);
     gb_free(A->colidx);
@@ -154,13 +161,13 @@ void gb_obj_free_storage(GB_Obj *A) {
 }
 
 int64_t gb_nvals(GB_Obj *A) {
-    if (A->kind == GB_KIND_MATRIX) return A->nvals;
+    if (A->kind == GB_KIND_MATRIX && !A->cw) return A->nvals;
     if (!A->nvals_valid) {
         int64_t v;
         if (A->pub && A->pub_seq && A->pub_epoch == gb_epoch() && gb_host_slot_wait(A->pub, A->pub_seq, &v)) {
             A->nvals = v;  // published by the kernel that produced d_nvals
         } else {
-            A->nvals = gb_read_i64(A->d_nvals);
+            A->nvals = gb_read_i64(A->cw ? A->cw_stat : A->d_nvals);
         }
         A->nvals_valid = true;
     }
@@ -170,6 +177,7 @@ int64_t gb_nvals(GB_Obj *A) {
 void gb_install_csr(GB_Obj *C, int64_t nrows, int64_t ncols, int64_t nvals, int64_t *rowptr,
                     int32_t *colidx, void *vals, bool iso) {
     if (C->kind == GB_KIND_MATRIX) {
+        gb_cw_release(C);
         gb_drop_transpose(C);
         gb_free(C->rowptr);
         gb_free(C->colidx);
@@ -1095,22 +1103,22 @@ GrB_Info GrB_Matrix_dup(GrB_Matrix *C, const GrB_Matrix A) {
 GrB_Info GrB_Matrix_clear(GrB_Matrix A) {
     GB_Obj *o = OBJ(A);
     return gb_api(o, [&] {
-        gb_obj_check(A);
+        gb_obj_check_raw(A);
         gb_obj_free_storage(o);
         alloc_empty_storage(o);
     });
 }
 GrB_Info GrB_Matrix_nrows(GrB_Index *n, const GrB_Matrix A) {
     if (!n) return GrB_NULL_POINTER;
-    return gb_api(OBJ(A), [&] { *n = gb_obj_check(A)->nrows; });
+    return gb_api(OBJ(A), [&] { *n = gb_obj_check_raw(A)->nrows; });
 }
 GrB_Info GrB_Matrix_ncols(GrB_Index *n, const GrB_Matrix A) {
     if (!n) return GrB_NULL_POINTER;
-    return gb_api(OBJ(A), [&] { *n = gb_obj_check(A)->ncols; });
+    return gb_api(OBJ(A), [&] { *n = gb_obj_check_raw(A)->ncols; });
 }
 GrB_Info GrB_Matrix_nvals(GrB_Index *n, const GrB_Matrix A) {
     if (!n) return GrB_NULL_POINTER;
-    return gb_api(OBJ(A), [&] { *n = gb_nvals(gb_obj_check(A)); });
+    return gb_api(OBJ(A), [&] { *n = gb_nvals(gb_obj_check_raw(A)); });
 }
 GrB_Info GrB_Matrix_resize(GrB_Matrix A, GrB_Index nrows, GrB_Index ncols) {
     return gb_api(OBJ(A), [&] {
@@ -1141,7 +1149,7 @@ GrB_Info GrB_Matrix_free(GrB_Matrix *A) {
 GrB_Info GrB_Matrix_wait(GrB_Matrix A, GrB_WaitMode mode) {
     (void)mode;
     return gb_api(OBJ(A), [&] {
-        gb_obj_check(A);
+        gb_obj_check_raw(A);
         gb_sync();
     });
 }
@@ -1153,7 +1161,7 @@ GrB_Info GrB_Matrix_error(const char **error, const GrB_Matrix A) {
 }
 GrB_Info GxB_Matrix_type(GrB_Type *type, const GrB_Matrix A) {
     if (!type) return GrB_NULL_POINTER;
-    return gb_api(OBJ(A), [&] { *type = gb_obj_check(A)->type; });
+    return gb_api(OBJ(A), [&] { *type = gb_obj_check_raw(A)->type; });
 }
 GrB_Info GrB_Matrix_removeElement(GrB_Matrix A, GrB_Index i, GrB_Index j) {
     return gb_api(OBJ(A), [&] {

@@ -915,8 +915,11 @@ extern "C" {
 GrB_Info GrB_mxm(GrB_Matrix C, const GrB_Matrix Mask, const GrB_BinaryOp accum, const GrB_Semiring op,
                  const GrB_Matrix A, const GrB_Matrix B, const GrB_Descriptor desc) {
     return gb_api(OBJ(C), [&] {
-        do_mxm(gb_obj_check(C), gb_obj_check(Mask, true), accum, op, gb_obj_check(A), gb_obj_check(B),
-               gb_read_desc(desc));
+        const gb_desc d = gb_read_desc(desc);
+        if (gb_colbits_mxm(gb_obj_check_raw(C), gb_obj_check_raw(Mask, true), accum, op, gb_obj_check_raw(A),
+                           gb_obj_check_raw(B), d))
+            return;
+        do_mxm(gb_obj_check(C), gb_obj_check(Mask, true), accum, op, gb_obj_check(A), gb_obj_check(B), d);
     });
 }
 
@@ -1144,6 +1147,10 @@ GrB_Info GrB_Semiring_new(GrB_Semiring *semiring, GrB_Monoid add, GrB_BinaryOp m
                                    const GrB_Index *I, GrB_Index ni, const GrB_Index *J, GrB_Index nj,       \
                                    const GrB_Descriptor desc) {                                              \
         return gb_api(OBJ(C), [&] {                                                                          \
+            const gb_desc d = gb_read_desc(desc);                                                            \
+            if (gb_colbits_assign_scalar(gb_obj_check_raw(C), gb_obj_check_raw(Mask, true), accum, &x,       \
+                                         GBAMD_T_##T, I, J, d))                                              \
+                return;                                                                                      \
             GB_Obj *Co = gb_obj_check(C);                                                                    \
             if (Co->kind != GB_KIND_MATRIX)                                                                  \
                 vector_assign_scalar(Co, gb_obj_check(Mask, true), accum, &x, GBAMD_T_##T, I, (int64_t)ni,   \
