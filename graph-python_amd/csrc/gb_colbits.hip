@@ -94,6 +94,10 @@ struct cb_step_args {
     const uint8_t *a_val, *b_val;           // iso values of the operands (nullptr: not iso)
     int mul;
     uint8_t *out_val;
+    const uint64_t *S_in;                   // F's summary: bit i = (F[i] != 0), valid when stat_in[2] == 1
+    uint64_t *S_out;                        // out's summary (zeroed)
+    const int32_t *p_tab, *s_tab;           // hub pieces (row, piece) of the pull / push orientation
+    int64_t p_nhub, s_nhub, H;
 };
 
 GB_DEV uint64_t cb_need(const cb_step_args &a, int64_t j, bool m_on) {
@@ -114,32 +118,76 @@ GB_DEV bool cb_mult_value(int mul, bool x, bool y) {
 }
 
 // One level of C<M> = F lor.land B (or any.pair ...): pull or push, chosen from
-// stat_in on the device.  All blocks call the grid sums once.
+// stat_in on the device.  Rows longer than H of the chosen orientation run as
+// H-edge pieces from the cached hub table (a wave per piece, results OR'ed in
+// with atomics) so an R-MAT hub does not serialise one wave; the rest run a lane
+// per row.  All blocks call the grid sums once.
 __global__ __launch_bounds__(CB_BLOCK) void k_cw_step(cb_step_args a) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const bool m_on = !a.m_iso || cb_nonzero(a.m_iso, a.m_iso_size);
     const bool push = a.srp && (a.dir == 2 || (a.dir == 0 && a.stat_in[1] * a.alpha < a.nnz));
+    // sparse frontier: test the summary bit (L2-resident) before gathering a word
+    const bool use_sum = a.S_in && a.stat_in[2] == 1 && a.stat_in[0] * 4 < a.nin;
+    const int64_t H = a.H;
     long long cnt = 0, hint = 0;
+    // OR bits into out[j] (out is zeroed): count the new bits, the column's edges when it
+    // turns non-empty, and its summary bit
+    auto put = [&](int64_t j, uint64_t nb) {
+        const uint64_t old = atomicOr((unsigned long long *)&a.out[j], (unsigned long long)nb);
+        const uint64_t add = nb & ~old;
+        cnt += __popcll(add);
+        if (old == 0 && add) {
+            atomicOr((unsigned long long *)&a.S_out[j >> 6], 1ULL << (j & 63));
+            if (a.srp && j < a.nin) hint += a.srp[j + 1] - a.srp[j];
+        }
+    };
+    auto gather = [&](int64_t i) -> uint64_t {
+        if (use_sum && !((a.S_in[i >> 6] >> (i & 63)) & 1ULL)) return 0ULL;
+        return a.F[i];
+    };
     if (!push) {
+        // hub pieces: rows of the pull orientation longer than H
+        for (int64_t t = wave; t < a.p_nhub; t += nwaves) {
+            const int64_t j = a.p_tab[2 * t], piece = a.p_tab[2 * t + 1];
+            const uint64_t need = cb_need(a, j, m_on);
+            if (!need) continue;
+            const int64_t beg = a.prp[j] + piece * H, rend = a.prp[j + 1];
+            const int64_t end = beg + H < rend ? beg + H : rend;
+            uint64_t acc = 0;
+            for (int64_t qb = beg; qb < end; qb += 256) {
+                uint64_t f = 0;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int64_t q = qb + lane + 64 * u;
+                    if (q < end) f |= gather(a.pci[q]);
+                }
+                acc |= cb_wave_or(f);
+                if ((acc & need) == need) break;
+            }
+            if (lane == 0 && (acc & need)) put(j, acc & need);
+        }
         for (int64_t base = wave * 64; base < a.nout; base += nwaves * 64) {
             const int64_t j = base + lane;
             uint64_t need = 0, acc = 0;
             int64_t p = 0, e = 0;
+            bool hub = false;
             if (j < a.nout) {
                 need = cb_need(a, j, m_on);
                 if (need) {
                     p = a.prp[j];
                     e = a.prp[j + 1];
+                    hub = a.p_tab && e - p > H;
+                    if (hub) p = e;
                 }
             }
             const int64_t lim = e < p + CB_CAP ? e : p + CB_CAP;
             while (p < lim) {
-                uint64_t f = a.F[a.pci[p]];
-                if (p + 1 < lim) f |= a.F[a.pci[p + 1]];
-                if (p + 2 < lim) f |= a.F[a.pci[p + 2]];
-                if (p + 3 < lim) f |= a.F[a.pci[p + 3]];
+                uint64_t f = gather(a.pci[p]);
+                if (p + 1 < lim) f |= gather(a.pci[p + 1]);
+                if (p + 2 < lim) f |= gather(a.pci[p + 2]);
+                if (p + 3 < lim) f |= gather(a.pci[p + 3]);
                 acc |= f;
                 p += 4;
                 if ((acc & need) == need) break;
@@ -157,19 +205,21 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cw_step(cb_step_args a) {
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
                         const int64_t q = qb + lane + 64 * u;
-                        if (q < eL) f |= a.F[a.pci[q]];
+                        if (q < eL) f |= gather(a.pci[q]);
                     }
                     aL |= cb_wave_or(f);
                     if ((aL & nL) == nL) break;
                 }
                 if (lane == L) acc = aL;
             }
-            if (j < a.nout) {
-                const uint64_t w = acc & need;
-                a.out[j] = w;
+            const uint64_t w = (j < a.nout && !hub) ? (acc & need) : 0ULL;
+            if (w) {
+                a.out[j] = w;  // hub columns are OR'ed in by their pieces
                 cnt += __popcll(w);
-                if (w && a.srp && j < a.nin) hint += a.srp[j + 1] - a.srp[j];
+                if (a.srp && j < a.nin) hint += a.srp[j + 1] - a.srp[j];
             }
+            const uint64_t sb = __ballot(w != 0);
+            if (lane == 0 && sb) atomicOr((unsigned long long *)&a.S_out[base >> 6], (unsigned long long)sb);
         }
     } else {
         auto push_one = [&](int64_t j, uint64_t f) {
@@ -177,11 +227,16 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cw_step(cb_step_args a) {
             if (!nb) return;
             const uint64_t cur = __hip_atomic_load(&a.out[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if ((cur & nb) == nb) return;
-            const uint64_t old = atomicOr((unsigned long long *)&a.out[j], (unsigned long long)nb);
-            const uint64_t add = nb & ~old;
-            cnt += __popcll(add);
-            if (old == 0 && add && j < a.nin) hint += a.srp[j + 1] - a.srp[j];
+            put(j, nb);
         };
+        for (int64_t t = wave; t < a.s_nhub; t += nwaves) {
+            const int64_t i = a.s_tab[2 * t], piece = a.s_tab[2 * t + 1];
+            const uint64_t f = a.F[i];
+            if (!f) continue;
+            const int64_t beg = a.srp[i] + piece * H, rend = a.srp[i + 1];
+            const int64_t end = beg + H < rend ? beg + H : rend;
+            for (int64_t q = beg + lane; q < end; q += 64) push_one(a.sci[q], f);
+        }
         for (int64_t base = wave * 64; base < a.nin; base += nwaves * 64) {
             const int64_t i = base + lane;
             const uint64_t f = i < a.nin ? a.F[i] : 0ULL;
@@ -189,6 +244,7 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cw_step(cb_step_args a) {
             if (f) {
                 p = a.srp[i];
                 e = a.srp[i + 1];
+                if (a.s_tab && e - p > H) p = e;  // a hub: its pieces above
             }
             const int64_t lim = e < p + CB_CAP ? e : p + CB_CAP;
             for (; p < lim; p++) push_one(a.sci[p], f);
@@ -208,8 +264,10 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cw_step(cb_step_args a) {
         cb_publish(a.pub, a.seq, tot);
     }
     if (gb_grid_sum(hint, a.gst2, &tot)) a.stat_out[1] = tot;
-    if (blockIdx.x == 0 && threadIdx.x == 0)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.stat_out[2] = 1;  // summary words valid
         *a.out_val = cb_mult_value(a.mul, a.a_val ? *a.a_val != 0 : true, a.b_val ? *a.b_val != 0 : true);
+    }
 }
 
 // stat[1] = out-edges (rows of srp) of the non-empty columns of F
@@ -226,7 +284,8 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cw_hint(const uint64_t *__restrict
 // CSR (k rows) -> column words; stat = [nvals, out-edges of the entries' columns in srp]
 __global__ __launch_bounds__(CB_BLOCK) void k_csr_to_cw(int k, int64_t nvals, const int64_t *__restrict__ rowptr,
                                                          const int32_t *__restrict__ colidx, const uint8_t *vals,
-                                                         int vsize, uint64_t *__restrict__ cw, uint8_t *cwv,
+                                                         int vsize, uint64_t *__restrict__ cw, uint64_t *__restrict__ S,
+                                                         uint8_t *cwv,
                                                          const int64_t *__restrict__ srp, int64_t nsrp,
                                                          int64_t *__restrict__ stat, unsigned long long *gst) {
     long long h = 0;
@@ -240,6 +299,7 @@ __global__ __launch_bounds__(CB_BLOCK) void k_csr_to_cw(int k, int64_t nvals, co
         }
         const int64_t j = colidx[e];
         atomicOr((unsigned long long *)&cw[j], 1ULL << lo);
+        atomicOr((unsigned long long *)&S[j >> 6], 1ULL << (j & 63));
         if (cwv) cb_copy(cwv + (j * k + lo) * vsize, vals + e * vsize, vsize);
         if (srp && j < nsrp) h += srp[j + 1] - srp[j];
     }
@@ -247,6 +307,7 @@ __global__ __launch_bounds__(CB_BLOCK) void k_csr_to_cw(int k, int64_t nvals, co
     if (gb_grid_sum(h, gst, &tot)) {
         stat[0] = nvals;
         stat[1] = tot;
+        stat[2] = 1;
     }
 }
 
@@ -272,16 +333,22 @@ __global__ void k_cw_fill(const uint64_t *__restrict__ cw, int64_t n, int k, con
 }
 
 // C<M> = x (all indices, no accum): bits OR'ed in, x stored at the mask's entries,
-// count delta added to stat[0]
+// count delta added to stat[0].  A wave owns 64 columns; the value stores of each
+// column with new bits go out as one wave-wide store (lane r -> row r), so a
+// column's values are written as one coalesced segment.
 __global__ __launch_bounds__(CB_BLOCK) void k_cw_assign(int64_t n, int k, const uint64_t *__restrict__ M,
                                                          const void *m_iso, int m_iso_size, const uint8_t *m_vals,
                                                          int m_vsize, uint64_t *__restrict__ C, uint8_t *cv,
                                                          unsigned long long x, int vsize, int64_t *stat,
                                                          unsigned long long *gst) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const bool m_on = !m_iso || cb_nonzero(m_iso, m_iso_size);
     long long delta = 0;
-    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
-        uint64_t m = m_on ? M[j] : 0ULL;
+    for (int64_t base = wave * 64; base < n; base += nwaves * 64) {
+        const int64_t j = base + lane;
+        uint64_t m = (m_on && j < n) ? M[j] : 0ULL;
         if (m && m_vals) {  // value mask: keep the bits whose value is nonzero
             uint64_t t = m, keep = 0;
             while (t) {
@@ -291,17 +358,20 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cw_assign(int64_t n, int k, const 
             }
             m = keep;
         }
-        if (!m) continue;
-        const uint64_t old = C[j];
-        C[j] = old | m;
-        delta += __popcll(m & ~old);
-        uint64_t t = m;
-        while (t) {
-            const int r = __ffsll((unsigned long long)t) - 1;
-            t &= t - 1;
-            cb_copy(cv + (j * k + r) * vsize, &x, vsize);
+        if (m) {
+            const uint64_t old = C[j];
+            C[j] = old | m;
+            delta += __popcll(m & ~old);
+        }
+        uint64_t cols = __ballot(m != 0);
+        while (cols) {
+            const int c = __ffsll((unsigned long long)cols) - 1;
+            cols &= cols - 1;
+            const uint64_t mc = cb_shfl(m, c);
+            if (lane < k && ((mc >> lane) & 1ULL)) cb_copy(cv + ((base + c) * k + lane) * vsize, &x, vsize);
         }
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0) stat[2] = 0;  // the summary words no longer match
     gb_grid_add(delta, (unsigned long long *)stat, gst);
 }
 
@@ -329,8 +399,9 @@ void to_cw(GB_Obj *A, const int64_t *srp, int64_t nsrp, const void *hint_key) {
     const int k = (int)A->nrows;
     const int64_t n = A->ncols, nv = A->nvals;
     const int vs = (int)A->type->size;
-    uint64_t *cw = gb_malloc_n<uint64_t>(n > 0 ? n : 1);
-    gb_memset(cw, 0, (n > 0 ? n : 1) * sizeof(uint64_t));
+    const int64_t nw = n + gb_words(n) + 1;  // words, then the summary bitmap
+    uint64_t *cw = gb_malloc_n<uint64_t>(nw);
+    gb_memset(cw, 0, nw * sizeof(uint64_t));
     int64_t *stat = gb_malloc_n<int64_t>(4);
     gb_memset(stat, 0, 4 * sizeof(int64_t));
     const bool iso = A->iso && nv > 0;
@@ -343,7 +414,7 @@ void to_cw(GB_Obj *A, const int64_t *srp, int64_t nsrp, const void *hint_key) {
     }
     if (nv > 0) {
         hipLaunchKernelGGL(k_csr_to_cw, dim3(cb_grid(nv, 2048)), dim3(CB_BLOCK), 0, gb_stream(), k, nv, A->rowptr,
-                           A->colidx, (const uint8_t *)A->vals, vs, cw, iso ? nullptr : (uint8_t *)cwv, srp, nsrp,
+                           A->colidx, (const uint8_t *)A->vals, vs, cw, cw + n, iso ? nullptr : (uint8_t *)cwv, srp, nsrp,
                            stat, grid_state(0));
         GB_LAUNCH_CHECK();
     }
@@ -488,10 +559,15 @@ bool gb_colbits_mxm(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, GrB_Semiring sr, G
         A->hint_valid = true;
         A->hint_key = sv.rowptr;
     }
-    uint64_t *out = gb_malloc_n<uint64_t>(bc > 0 ? bc : 1);
+    const int64_t onw = bc + gb_words(bc) + 1;  // words, then the summary bitmap
+    uint64_t *out = gb_malloc_n<uint64_t>(onw);
     int64_t *stat = gb_malloc_n<int64_t>(4);
     uint8_t *oval = (uint8_t *)gb_malloc(1);
-    if (dir != 1) GB_HIP(hipMemsetAsync(out, 0, (bc > 0 ? bc : 1) * sizeof(uint64_t), gb_stream()));
+    GB_HIP(hipMemsetAsync(out, 0, onw * sizeof(uint64_t), gb_stream()));
+    int64_t H = gb_knob("colbits_hub");
+    if (H <= 0) H = 512;
+    gb_view_hubs(pv, B, d.tran1 ? 0 : 1, H);
+    if (dir != 1) gb_view_hubs(sv, B, d.tran1 ? 1 : 0, H);
     if (!C->pub) C->pub = gb_host_slot_alloc();
     const uint64_t seq = gb_next_pub_seq();
 
@@ -523,6 +599,13 @@ bool gb_colbits_mxm(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, GrB_Semiring sr, G
     a.b_val = (uses_b && B->iso) ? (const uint8_t *)B->vals : nullptr;
     a.mul = mul;
     a.out_val = oval;
+    a.S_in = A->cw + inner;
+    a.S_out = out + bc;
+    a.p_tab = pv.hubs;
+    a.p_nhub = pv.hubs ? pv.nhubs : 0;
+    a.s_tab = (dir != 1) ? sv.hubs : nullptr;
+    a.s_nhub = (dir != 1 && sv.hubs) ? sv.nhubs : 0;
+    a.H = H;
     // enough waves to cover the output in a few chunks each; every block joins the grid sums
     hipLaunchKernelGGL(k_cw_step, dim3(cb_grid((bc > inner ? bc : inner), 2048)), dim3(CB_BLOCK), 0, gb_stream(), a);
     GB_LAUNCH_CHECK();
