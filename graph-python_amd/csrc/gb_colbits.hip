@@ -36,7 +36,8 @@
 namespace {
 
 constexpr int CB_BLOCK = 256;
-constexpr int CB_CAP = 32;  // edges a lane walks alone before the wave takes its column over
+constexpr int CB_CAP = 32;  // edges a lane walks alone before the wave takes its column over (push)
+constexpr int CB_U = 4;     // 64-edge windows a pull wave has in flight
 
 GB_DEV uint64_t cb_shfl(uint64_t v, int src) {
     const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
@@ -168,51 +169,79 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cw_step(cb_step_args a) {
             }
             if (lane == 0 && (acc & need)) put(j, acc & need);
         }
+        // a wave owns 64 consecutive output columns and walks their (non-hub) in-edges as
+        // one flat list: edge t of the list belongs to the column found by a shuffle binary
+        // search over the columns' list offsets; gathers are OR-folded by a segmented wave
+        // scan and the segment ends fold into the column's LDS slot.  Columns whose need is
+        // empty (visited by every source) contribute no edges.
+        __shared__ uint64_t lacc[CB_BLOCK / 64][64];
+        uint64_t *acc_w = lacc[threadIdx.x >> 6];
         for (int64_t base = wave * 64; base < a.nout; base += nwaves * 64) {
             const int64_t j = base + lane;
-            uint64_t need = 0, acc = 0;
-            int64_t p = 0, e = 0;
+            uint64_t need = 0;
+            int64_t s0 = 0;
+            int len = 0;
             bool hub = false;
             if (j < a.nout) {
                 need = cb_need(a, j, m_on);
                 if (need) {
-                    p = a.prp[j];
-                    e = a.prp[j + 1];
-                    hub = a.p_tab && e - p > H;
-                    if (hub) p = e;
+                    s0 = a.prp[j];
+                    const int64_t dl = a.prp[j + 1] - s0;
+                    hub = a.p_tab && dl > H;
+                    len = hub ? 0 : (int)dl;
                 }
             }
-            const int64_t lim = e < p + CB_CAP ? e : p + CB_CAP;
-            while (p < lim) {
-                uint64_t f = gather(a.pci[p]);
-                if (p + 1 < lim) f |= gather(a.pci[p + 1]);
-                if (p + 2 < lim) f |= gather(a.pci[p + 2]);
-                if (p + 3 < lim) f |= gather(a.pci[p + 3]);
-                acc |= f;
-                p += 4;
-                if ((acc & need) == need) break;
+            // exclusive scan of the lengths
+            int v = len;
+            for (int off = 1; off < 64; off <<= 1) {
+                const int g = __shfl_up(v, off, 64);
+                if (lane >= off) v += g;
             }
-            const bool more = (acc & need) != need && p < e;
-            uint64_t longs = __ballot(more);
-            while (longs) {
-                const int L = __ffsll((unsigned long long)longs) - 1;
-                longs &= longs - 1;
-                const int64_t pL = cb_shfl_i64(p, L), eL = cb_shfl_i64(e, L);
-                const uint64_t nL = cb_shfl(need, L);
-                uint64_t aL = cb_shfl(acc, L);
-                for (int64_t qb = pL; qb < eL; qb += 256) {
-                    uint64_t f = 0;
+            const int T = __shfl(v, 63, 64);
+            v -= len;
+            const int64_t eb = s0 - v;  // edge index = t + eb of the owning column
+            acc_w[lane] = 0;
+            for (int tb = 0; tb < T; tb += 64 * CB_U) {
+                // CB_U windows of 64 list positions: searches, then all loads, then the folds
+                int c[CB_U];
+                uint64_t f[CB_U];
 #pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const int64_t q = qb + lane + 64 * u;
-                        if (q < eL) f |= gather(a.pci[q]);
-                    }
-                    aL |= cb_wave_or(f);
-                    if ((aL & nL) == nL) break;
+                for (int u = 0; u < CB_U; u++) {
+                    const int t = tb + 64 * u + lane;
+                    // every lane runs the search (uniform shuffles); lanes past the list get c = 64
+                    const int tt = t < T ? t : T - 1;
+                    int lo = 0;
+#pragma unroll
+                    for (int step = 32; step > 0; step >>= 1)
+                        if (__shfl(v, lo + step, 64) <= tt) lo += step;
+                    c[u] = t < T ? lo : 64;
+                    f[u] = 0;
                 }
-                if (lane == L) acc = aL;
+                int32_t src[CB_U];
+#pragma unroll
+                for (int u = 0; u < CB_U; u++) {
+                    const int t = tb + 64 * u + lane;
+                    const int64_t q = (int64_t)t + cb_shfl_i64(eb, c[u] < 64 ? c[u] : 0);
+                    src[u] = t < T ? a.pci[q] : -1;
+                }
+#pragma unroll
+                for (int u = 0; u < CB_U; u++)
+                    if (src[u] >= 0) f[u] = gather(src[u]);
+#pragma unroll
+                for (int u = 0; u < CB_U; u++) {
+                    uint64_t x = f[u];
+                    const int cu = c[u];
+                    for (int off = 1; off < 64; off <<= 1) {
+                        const uint32_t glo = (uint32_t)__shfl_up((int)(uint32_t)x, off, 64);
+                        const uint32_t ghi = (uint32_t)__shfl_up((int)(uint32_t)(x >> 32), off, 64);
+                        const int cc = __shfl_up(cu, off, 64);
+                        if (lane >= off && cc == cu) x |= ((uint64_t)ghi << 32) | glo;
+                    }
+                    const int cn = __shfl_down(cu, 1, 64);
+                    if (cu < 64 && (lane == 63 || cn != cu)) acc_w[cu] |= x;
+                }
             }
-            const uint64_t w = (j < a.nout && !hub) ? (acc & need) : 0ULL;
+            const uint64_t w = (j < a.nout && !hub) ? (acc_w[lane] & need) : 0ULL;
             if (w) {
                 a.out[j] = w;  // hub columns are OR'ed in by their pieces
                 cnt += __popcll(w);
