@@ -65,9 +65,10 @@ GB_DEV void cb_copy(void *dst, const void *src, int size) {
         default: *(uint64_t *)dst = *(const uint64_t *)src; break;
     }
 }
-GB_DEV void cb_publish(gb_host_slot *pub, long long seq, long long value) {
+GB_DEV void cb_publish(gb_host_slot *pub, long long seq, long long value, long long hint) {
     if (!pub) return;
     __hip_atomic_store(&pub->value, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&pub->pad[0], hint, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __threadfence_system();
     __hip_atomic_store(&pub->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -117,6 +118,86 @@ GB_DEV bool cb_mult_value(int mul, bool x, bool y) {
         default: return x && y;  // LAND, TIMES, MIN
     }
 }
+
+// Pull of one wave's 64 output columns j = base + lane: their (non-hub) in-edges
+// are walked as one flat list -- list position t belongs to the column found by a
+// shuffle binary search over the columns' list offsets -- CB_U windows of 64 gathers
+// in flight, OR-folded by a segmented wave scan; the segment ends fold into the
+// columns' LDS slots acc_w[0..63].  Columns whose need is empty contribute no edges.
+// rp/ci: the pull rows (int64 or int32 row pointers, entries relative to ci).
+template <class RP>
+GB_DEV void cb_pull_chunk(const cb_step_args &a, int64_t j, bool m_on, bool use_sum, const RP *__restrict__ rp,
+                          const int32_t *__restrict__ ci, bool hubs, int64_t H, uint64_t *acc_w, uint64_t &need,
+                          bool &hub) {
+    const int lane = threadIdx.x & 63;
+    auto gather = [&](int64_t i) -> uint64_t {
+        if (use_sum && !((a.S_in[i >> 6] >> (i & 63)) & 1ULL)) return 0ULL;
+        return a.F[i];
+    };
+    int64_t s0 = 0;
+    int len = 0;
+    if (j < a.nout) {
+        need = cb_need(a, j, m_on);
+        if (need) {
+            s0 = rp[j];
+            const int64_t dl = (int64_t)rp[j + 1] - s0;
+            hub = hubs && dl > H;
+            len = hub ? 0 : (int)dl;
+        }
+    }
+    // exclusive scan of the lengths
+    int v = len;
+    for (int off = 1; off < 64; off <<= 1) {
+        const int g = __shfl_up(v, off, 64);
+        if (lane >= off) v += g;
+    }
+    const int T = __shfl(v, 63, 64);
+    v -= len;
+    const int64_t eb = s0 - v;  // edge index = t + eb of the owning column
+    acc_w[lane] = 0;
+    for (int tb = 0; tb < T; tb += 64 * CB_U) {
+        // CB_U windows of 64 list positions: searches, then all loads, then the folds
+        int c[CB_U];
+        uint64_t f[CB_U];
+#pragma unroll
+        for (int u = 0; u < CB_U; u++) {
+            const int t = tb + 64 * u + lane;
+            // every lane runs the search (uniform shuffles); lanes past the list get c = 64
+            const int tt = t < T ? t : T - 1;
+            int lo = 0;
+#pragma unroll
+            for (int step = 32; step > 0; step >>= 1)
+                if (__shfl(v, lo + step, 64) <= tt) lo += step;
+            c[u] = t < T ? lo : 64;
+            f[u] = 0;
+        }
+        int32_t src[CB_U];
+#pragma unroll
+        for (int u = 0; u < CB_U; u++) {
+            const int t = tb + 64 * u + lane;
+            const int64_t q = (int64_t)t + cb_shfl_i64(eb, c[u] < 64 ? c[u] : 0);
+            src[u] = t < T ? ci[q] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < CB_U; u++)
+            if (src[u] >= 0) f[u] = gather(src[u]);
+#pragma unroll
+        for (int u = 0; u < CB_U; u++) {
+            uint64_t x = f[u];
+            const int cu = c[u];
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t glo = (uint32_t)__shfl_up((int)(uint32_t)x, off, 64);
+                const uint32_t ghi = (uint32_t)__shfl_up((int)(uint32_t)(x >> 32), off, 64);
+                const int cc = __shfl_up(cu, off, 64);
+                if (lane >= off && cc == cu) x |= ((uint64_t)ghi << 32) | glo;
+            }
+            const int cn = __shfl_down(cu, 1, 64);
+            if (cu < 64 && (lane == 63 || cn != cu)) acc_w[cu] |= x;
+        }
+    }
+}
+
+GB_DEV void cb_finish(const cb_step_args &a, long long cnt, long long hint);
 
 // One level of C<M> = F lor.land B (or any.pair ...): pull or push, chosen from
 // stat_in on the device.  Rows longer than H of the chosen orientation run as
@@ -179,68 +260,8 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cw_step(cb_step_args a) {
         for (int64_t base = wave * 64; base < a.nout; base += nwaves * 64) {
             const int64_t j = base + lane;
             uint64_t need = 0;
-            int64_t s0 = 0;
-            int len = 0;
             bool hub = false;
-            if (j < a.nout) {
-                need = cb_need(a, j, m_on);
-                if (need) {
-                    s0 = a.prp[j];
-                    const int64_t dl = a.prp[j + 1] - s0;
-                    hub = a.p_tab && dl > H;
-                    len = hub ? 0 : (int)dl;
-                }
-            }
-            // exclusive scan of the lengths
-            int v = len;
-            for (int off = 1; off < 64; off <<= 1) {
-                const int g = __shfl_up(v, off, 64);
-                if (lane >= off) v += g;
-            }
-            const int T = __shfl(v, 63, 64);
-            v -= len;
-            const int64_t eb = s0 - v;  // edge index = t + eb of the owning column
-            acc_w[lane] = 0;
-            for (int tb = 0; tb < T; tb += 64 * CB_U) {
-                // CB_U windows of 64 list positions: searches, then all loads, then the folds
-                int c[CB_U];
-                uint64_t f[CB_U];
-#pragma unroll
-                for (int u = 0; u < CB_U; u++) {
-                    const int t = tb + 64 * u + lane;
-                    // every lane runs the search (uniform shuffles); lanes past the list get c = 64
-                    const int tt = t < T ? t : T - 1;
-                    int lo = 0;
-#pragma unroll
-                    for (int step = 32; step > 0; step >>= 1)
-                        if (__shfl(v, lo + step, 64) <= tt) lo += step;
-                    c[u] = t < T ? lo : 64;
-                    f[u] = 0;
-                }
-                int32_t src[CB_U];
-#pragma unroll
-                for (int u = 0; u < CB_U; u++) {
-                    const int t = tb + 64 * u + lane;
-                    const int64_t q = (int64_t)t + cb_shfl_i64(eb, c[u] < 64 ? c[u] : 0);
-                    src[u] = t < T ? a.pci[q] : -1;
-                }
-#pragma unroll
-                for (int u = 0; u < CB_U; u++)
-                    if (src[u] >= 0) f[u] = gather(src[u]);
-#pragma unroll
-                for (int u = 0; u < CB_U; u++) {
-                    uint64_t x = f[u];
-                    const int cu = c[u];
-                    for (int off = 1; off < 64; off <<= 1) {
-                        const uint32_t glo = (uint32_t)__shfl_up((int)(uint32_t)x, off, 64);
-                        const uint32_t ghi = (uint32_t)__shfl_up((int)(uint32_t)(x >> 32), off, 64);
-                        const int cc = __shfl_up(cu, off, 64);
-                        if (lane >= off && cc == cu) x |= ((uint64_t)ghi << 32) | glo;
-                    }
-                    const int cn = __shfl_down(cu, 1, 64);
-                    if (cu < 64 && (lane == 63 || cn != cu)) acc_w[cu] |= x;
-                }
-            }
+            cb_pull_chunk(a, j, m_on, use_sum, a.prp, a.pci, a.p_tab != nullptr, H, acc_w, need, hub);
             const uint64_t w = (j < a.nout && !hub) ? (acc_w[lane] & need) : 0ULL;
             if (w) {
                 a.out[j] = w;  // hub columns are OR'ed in by their pieces
@@ -287,16 +308,87 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cw_step(cb_step_args a) {
             }
         }
     }
+    cb_finish(a, cnt, hint);
+}
+
+// count and edge-hint grid sums; whichever block finishes the second one publishes
+// both to the host mailbox (the hint lets the host pick the next call's direction)
+GB_DEV void cb_finish(const cb_step_args &a, long long cnt, long long hint) {
     long long tot;
+    int nf = 0;
     if (gb_grid_sum(cnt, a.gst, &tot)) {
-        a.stat_out[0] = tot;
-        cb_publish(a.pub, a.seq, tot);
+        __hip_atomic_store(&a.stat_out[0], (int64_t)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        nf++;
     }
-    if (gb_grid_sum(hint, a.gst2, &tot)) a.stat_out[1] = tot;
+    if (gb_grid_sum(hint, a.gst2, &tot)) {
+        __hip_atomic_store(&a.stat_out[1], (int64_t)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        nf++;
+    }
+    if (nf) {
+        __threadfence();
+        unsigned long long *flag = a.gst + (size_t)GB_GRID_SHARDS * GB_GRID_STRIDE + 8;
+        const unsigned long long old = atomicAdd(flag, (unsigned long long)nf);
+        if (old + nf == 2) {
+            atomicExch(flag, 0ULL);
+            __threadfence();
+            const long long c = __hip_atomic_load(&a.stat_out[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const long long h = __hip_atomic_load(&a.stat_out[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            cb_publish(a.pub, a.seq, c, h);
+        }
+    }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         a.stat_out[2] = 1;  // summary words valid
         *a.out_val = cb_mult_value(a.mul, a.a_val ? *a.a_val != 0 : true, a.b_val ? *a.b_val != 0 : true);
     }
+}
+
+// XCD-sliced pull: blocks b with b % 8 == c (dispatched to XCD c) walk only the
+// in-edges whose source lies in column slice c of the pull CSR (the cached slice-major
+// copy, gb_spmv_sliced.hip), so their F gathers stay inside one n/8-word range that
+// the XCD's L2 holds; each slice writes its partial words, k_cw_combine ORs them.
+__global__ __launch_bounds__(CB_BLOCK) void k_cw_pull_sl(cb_step_args a, const int32_t *__restrict__ srp,
+                                                          const int32_t *__restrict__ scol,
+                                                          const int64_t *__restrict__ sbase, uint64_t *part) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int c = blockIdx.x % 8;
+    const int64_t wave = (int64_t)(blockIdx.x / 8) * (CB_BLOCK / 64) + wid;
+    const int64_t nwaves = (int64_t)(gridDim.x / 8) * (CB_BLOCK / 64);
+    const bool m_on = !a.m_iso || cb_nonzero(a.m_iso, a.m_iso_size);
+    const bool use_sum = a.S_in && a.stat_in[2] == 1 && a.stat_in[0] * 4 < a.nin;
+    const int32_t *rp = srp + (int64_t)c * (a.nout + 1);
+    const int32_t *ci = scol + sbase[c];
+    uint64_t *pc = part + (int64_t)c * a.nout;
+    __shared__ uint64_t lacc[CB_BLOCK / 64][64];
+    uint64_t *acc_w = lacc[wid];
+    for (int64_t base = wave * 64; base < a.nout; base += nwaves * 64) {
+        const int64_t j = base + lane;
+        uint64_t need = 0;
+        bool hub = false;
+        cb_pull_chunk(a, j, m_on, use_sum, rp, ci, false, 0, acc_w, need, hub);
+        if (j < a.nout) pc[j] = acc_w[lane] & need;
+    }
+}
+
+// out[j] = OR of the 8 slices' partial words; count, edge hint, summary, publish
+__global__ __launch_bounds__(CB_BLOCK) void k_cw_combine(cb_step_args a, const uint64_t *__restrict__ part) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    long long cnt = 0, hint = 0;
+    for (int64_t base = wave * 64; base < a.nout; base += nwaves * 64) {
+        const int64_t j = base + lane;
+        uint64_t w = 0;
+        if (j < a.nout) {
+#pragma unroll
+            for (int c = 0; c < 8; c++) w |= part[(int64_t)c * a.nout + j];
+            a.out[j] = w;
+            cnt += __popcll(w);
+            if (w && a.srp && j < a.nin) hint += a.srp[j + 1] - a.srp[j];
+        }
+        const uint64_t sb = __ballot(w != 0);
+        if (lane == 0) a.S_out[base >> 6] = sb;
+    }
+    cb_finish(a, cnt, hint);
 }
 
 // stat[1] = out-edges (rows of srp) of the non-empty columns of F
@@ -635,9 +727,40 @@ bool gb_colbits_mxm(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, GrB_Semiring sr, G
     a.s_tab = (dir != 1) ? sv.hubs : nullptr;
     a.s_nhub = (dir != 1 && sv.hubs) ? sv.nhubs : 0;
     a.H = H;
-    // enough waves to cover the output in a few chunks each; every block joins the grid sums
-    hipLaunchKernelGGL(k_cw_step, dim3(cb_grid((bc > inner ? bc : inner), 2048)), dim3(CB_BLOCK), 0, gb_stream(), a);
-    GB_LAUNCH_CHECK();
+    // host-side direction when the producer of A published its edge hint (the BFS loop
+    // has read A's count from the same mailbox): pull then runs XCD-sliced
+    bool sliced_pull = false;
+    // measured slower at R-MAT s22 (0.96-1.0 ms vs 0.85-0.90 ms per pull level): opt-in
+    int64_t sl_knob = gb_knob("colbits_sliced");  // 0 never, 1 always (pull), 3 when the host knows it pulls
+    sl_knob = sl_knob == 0 ? 2 : sl_knob == 3 ? 0 : sl_knob;
+    if (sl_knob != 2 && dir != 2 && bc >= 64 * 8 && (sl_knob == 1 || dir == 1)) {
+        sliced_pull = true;
+    } else if (sl_knob != 2 && dir != 2 && A->pub && A->pub_seq && A->hint_valid &&
+               A->hint_key == (const void *)sv.rowptr && bc >= 64 * 8) {
+        const long long seq_now = __atomic_load_n(&A->pub->seq, __ATOMIC_ACQUIRE);
+        if (seq_now == (long long)A->pub_seq) {
+            const long long h = __atomic_load_n(&A->pub->pad[0], __ATOMIC_RELAXED);
+            sliced_pull = dir == 1 || sl_knob == 1 || !(h * a.alpha < a.nnz);
+        }
+    }
+    if (sliced_pull) gb_view_slices(pv, B, d.tran1 ? 0 : 1);
+    if (sliced_pull && pv.sl_colidx) {
+        gb_scratch s;
+        uint64_t *part = s.get<uint64_t>((size_t)8 * bc);
+        unsigned g = cb_grid(bc, 2048);
+        g = (g + 7) / 8 * 8;
+        hipLaunchKernelGGL(k_cw_pull_sl, dim3(g), dim3(CB_BLOCK), 0, gb_stream(), a, pv.sl_rowptr, pv.sl_colidx,
+                           pv.sl_base, part);
+        GB_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_cw_combine, dim3(cb_grid(bc, 2048)), dim3(CB_BLOCK), 0, gb_stream(), a,
+                           (const uint64_t *)part);
+        GB_LAUNCH_CHECK();
+    } else {
+        // enough waves to cover the output in a few chunks each; every block joins the grid sums
+        hipLaunchKernelGGL(k_cw_step, dim3(cb_grid((bc > inner ? bc : inner), 2048)), dim3(CB_BLOCK), 0, gb_stream(),
+                           a);
+        GB_LAUNCH_CHECK();
+    }
 
     // install into C (stream-ordered frees: the kernel has read A/M before they go)
     if (C->kind == GB_KIND_MATRIX && !C->cw) {

@@ -62,7 +62,8 @@ def _msbfs(gb, A, roots, n):
 @pytest.mark.parametrize("k", [1, 7, 64])
 @pytest.mark.parametrize("direction", [0, 1, 2])  # auto (device-chosen), pull only, push only
 @pytest.mark.parametrize("hub", [0, 8])  # hub pieces of the default 512 edges, or of 8 (most rows)
-def test_msbfs_rmat_vs_oracle(gb, scale, k, direction, hub):
+@pytest.mark.parametrize("sliced", [0, 1, 3])  # pull XCD-sliced: never (default) / always / when the host knows it pulls
+def test_msbfs_rmat_vs_oracle(gb, scale, k, direction, hub, sliced):
     G = O.rmat(scale, 16, 42)
     n = G.nrows
     r, c, _ = G.to_coo()
@@ -71,7 +72,7 @@ def test_msbfs_rmat_vs_oracle(gb, scale, k, direction, hub):
     deg = np.diff(G.indptr)
     roots = rng.choice(np.flatnonzero(deg > 0), k, replace=False)
     roots[0] = int(np.argmax(deg))  # the hub: long columns go to the wave path
-    with _knobs(gb, colbits=1, colbits_direction=direction, colbits_hub=hub):
+    with _knobs(gb, colbits=1, colbits_direction=direction, colbits_hub=hub, colbits_sliced=sliced):
         got, _ = _msbfs(gb, A, roots, n)
     for i, src in enumerate(roots):
         lev, _, _ = O.bfs_levels(G, int(src))
