@@ -757,8 +757,9 @@ bool gb_colbits_mxm(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, GrB_Semiring sr, G
         GB_LAUNCH_CHECK();
     } else {
         // enough waves to cover the output in a few chunks each; every block joins the grid sums
-        hipLaunchKernelGGL(k_cw_step, dim3(cb_grid((bc > inner ? bc : inner), 2048)), dim3(CB_BLOCK), 0, gb_stream(),
-                           a);
+        const int64_t gcap = gb_knob("colbits_grid");
+        hipLaunchKernelGGL(k_cw_step, dim3(cb_grid((bc > inner ? bc : inner), gcap > 0 ? (unsigned)gcap : 2048)),
+                           dim3(CB_BLOCK), 0, gb_stream(), a);
         GB_LAUNCH_CHECK();
     }
 
