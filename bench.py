@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-secondary", action="store_true", help="skip the config 2 / config 4 lines")
     p.add_argument("--no-msbfs", action="store_true", help="skip the multi-source (masked mxm) BFS line")
+    p.add_argument("--msbfs-sharded", action="store_true", help="N > 1: add the row-sharded multi-source BFS line")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     # rehearsal of the N>1 path on one GPU: all ranks on one device, gloo transport
@@ -202,6 +203,113 @@ def config3_msbfs(lib, torch, stream, O, args, A, n, ap, ai, deg, roots16):
                         f"(GrB_Matrix_assign + masked GrB_mxm, Q/V {K} x n), R-MAT s{args.scale}",
             "roots": K, "levels": levels, "ms_per_batch": el * 1e3, "gteps": edges / el / 1e9,
             "edges": edges, "parity_vs_oracle_2_roots": parity}
+
+
+def config3_msbfs_sharded(lib, torch, stream, O, args, dist, world, rank, AT, part, deg, roots16):
+    """The 64-root batched BFS 1-D row-sharded (north_star's mxm sharding): rank r holds
+    rows [lo, hi) of A^T and per level computes its slice of every root's next frontier,
+        Vloc<Qloc.V> = d;  Qloc<!Vloc.S, replace> = Q lor.land (A^T shard)^T   (GrB_DESC_RSCT1)
+    then the slices' column words (8 B per vertex: all 64 roots' bits) are all-gathered
+    straight into Q's words (GxB_Matrix_colwords_view / _touch) -- one collective per level
+    for all 64 roots.  Opt-in (--msbfs-sharded)."""
+    from graphblas_amd import device as gdev
+    from graphblas_amd import dist as gdist
+
+    K = 64
+    n = 1 << args.scale
+    lo, hi = part["lo"], part["hi"]
+    nloc = hi - lo
+    rng = np.random.default_rng(args.seed + 1)
+    pool = np.setdiff1d(np.flatnonzero(deg > 0), roots16)
+    roots = np.concatenate([roots16, rng.choice(pool, K - len(roots16), replace=False)]).astype(np.uint64)
+    mine = (roots >= lo) & (roots < hi)
+    li, lj = np.flatnonzero(mine).astype(np.uint64), (roots[mine] - lo).astype(np.uint64)
+    Q, Ql, Vl = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+    ok(lib.GrB_Matrix_new(ctypes.byref(Q), lib.GrB_BOOL, K, n), "Q")
+    ok(lib.GrB_Matrix_new(ctypes.byref(Ql), lib.GrB_BOOL, K, nloc), "Qloc")
+    ok(lib.GrB_Matrix_new(ctypes.byref(Vl), lib.GrB_INT32, K, nloc), "Vloc")
+    qi = np.arange(K, dtype=np.uint64)
+    vslot = part["slot"] * 64  # vertices per rank slot (words exchanged per rank)
+    ex = gdist.BitmapAllGather(dist, {"slot": vslot}, world, "cuda")
+    zero_copy = vslot * world == n and args.dist_backend == "nccl"
+    nv = ctypes.c_uint64()
+    sr, desc, ALL = lib.GrB_LOR_LAND_SEMIRING_BOOL, lib.GrB_DESC_RSCT1, lib.GrB_ALL
+
+    def exchange():
+        ptr, cnt = gdev.colwords_view(Ql)
+        with torch.cuda.stream(stream):
+            ex.send[:cnt].copy_(gdev.device_tensor(torch, ptr, cnt))
+            qptr, qn = gdev.colwords_view(Q)
+            qw = gdev.device_tensor(torch, qptr, qn)
+            if zero_copy:
+                ex.run(qw)
+            else:
+                g = ex.run()
+                qw.copy_(g[:qn])
+        ok(lib.GxB_Matrix_colwords_touch(Q), "touch Q")
+
+    def batch():
+        ok(lib.GrB_Matrix_clear(Q), "clear Q")
+        ok(lib.GrB_Matrix_clear(Ql), "clear Qloc")
+        ok(lib.GrB_Matrix_clear(Vl), "clear Vloc")
+        ok(lib.GxB_Matrix_build_Scalar_BOOL(Q, ctypes.c_void_p(qi.ctypes.data), ctypes.c_void_p(roots.ctypes.data),
+                                            True, K), "build Q")
+        if li.size:
+            ok(lib.GxB_Matrix_build_Scalar_BOOL(Ql, ctypes.c_void_p(li.ctypes.data), ctypes.c_void_p(lj.ctypes.data),
+                                                True, li.size), "build Qloc")
+        d = 0
+        while True:
+            d += 1
+            ok(lib.GrB_Matrix_assign_INT32(Vl, Ql, None, d, ALL, K, ALL, nloc, None), "Vloc<Qloc> = d")
+            ok(lib.GrB_mxm(Ql, Vl, None, sr, Q, AT, desc), "Qloc<!Vloc.S> = Q lor.land AT'")
+            exchange()
+            ok(lib.GrB_Matrix_nvals(ctypes.byref(nv), Q), "nvals")
+            if nv.value == 0:
+                return d
+
+    levels = batch()
+    # parity (row 0 = the first headline root) and reached edges, gathered over ranks
+    ok(lib.GrB_Matrix_nvals(ctypes.byref(nv), Vl), "nvals Vloc")
+    m = nv.value
+    vi, vj, vx = np.empty(m, np.uint64), np.empty(m, np.uint64), np.empty(m, np.int32)
+    cnt = ctypes.c_uint64(m)
+    ok(lib.GrB_Matrix_extractTuples_INT32(ctypes.c_void_p(vi.ctypes.data), ctypes.c_void_p(vj.ctypes.data),
+                                          ctypes.c_void_p(vx.ctypes.data), ctypes.byref(cnt), Vl), "extract Vloc")
+    vi, vj = vi.astype(np.int64), vj.astype(np.int64) + lo
+    dev = "cuda" if args.dist_backend == "nccl" else "cpu"
+    e_t = torch.tensor([int(deg[vj].sum())], dtype=torch.int64, device=dev)
+    dist.all_reduce(e_t)
+    edges = int(e_t.item())
+    row0 = torch.zeros(vslot, dtype=torch.int32)
+    sel = vi == 0
+    row0[torch.from_numpy(vj[sel] - lo)] = torch.from_numpy(vx[sel])
+    allv = [torch.zeros_like(row0).to(dev) for _ in range(world)]
+    dist.all_gather(allv, row0.to(dev))
+    parity = None
+    if rank == 0:
+        got = torch.cat([t.cpu() for t in allv]).numpy()[:n]
+        lev, _, _ = O.bfs_levels(O.rmat(args.scale, args.edge_factor, args.seed), int(roots[0]))
+        parity = bool(np.array_equal(got, lev))
+    for _ in range(2):
+        batch()
+    torch.cuda.synchronize()
+    dist.barrier()
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        batch()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = (time.perf_counter() - t0) / reps
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    for h in (Q, Ql, Vl):
+        ok(lib.GrB_Matrix_free(ctypes.byref(h)), "free")
+    return {"workload": f"multi-source level BFS, {K} roots at once, 1-D row shards x{world}: Vloc<Qloc.V> = d; "
+                        f"Qloc<!Vloc.S,replace> = Q lor.land (A^T shard)^T, column words all-gathered per level",
+            "roots": K, "levels": levels, "ms_per_batch": el * 1e3, "gteps": edges / el / 1e9, "edges": edges,
+            "parity_vs_oracle_root0": parity, "zero_copy": zero_copy}
 
 
 def config2_spmv(lib, torch, stream, args, scale, ef):
@@ -684,6 +792,9 @@ def main():
         del xs, ys
 
     secondary = {}
+    if world > 1 and args.msbfs_sharded:
+        secondary["config3_msbfs_64_roots_sharded"] = config3_msbfs_sharded(
+            lib, torch, stream, O, args, dist, world, rank, A, part, deg, roots)
     if rank == 0 and world == 1 and not args.no_msbfs:
         secondary["config3_msbfs_64_roots"] = config3_msbfs(lib, torch, stream, O, args, A, n, ap, ai, deg, roots)
     if rank == 0 and world == 1 and not args.no_secondary:

@@ -496,6 +496,30 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cw_assign(int64_t n, int k, const 
     gb_grid_add(delta, (unsigned long long *)stat, gst);
 }
 
+// count + summary of rewritten words; publish the count
+__global__ __launch_bounds__(CB_BLOCK) void k_cw_recount(const uint64_t *__restrict__ W, int64_t n,
+                                                          uint64_t *__restrict__ S, int64_t *stat,
+                                                          unsigned long long *gst, gb_host_slot *pub, long long seq) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    long long cnt = 0;
+    for (int64_t base = wave * 64; base < n; base += nwaves * 64) {
+        const int64_t j = base + lane;
+        const uint64_t w = j < n ? W[j] : 0ULL;
+        cnt += __popcll(w);
+        const uint64_t sb = __ballot(w != 0);
+        if (lane == 0) S[base >> 6] = sb;
+    }
+    long long tot;
+    if (gb_grid_sum(cnt, gst, &tot)) {
+        stat[0] = tot;
+        stat[1] = 0;
+        stat[2] = 1;
+        cb_publish(pub, seq, tot, 0);
+    }
+}
+
 // dense fill of an iso value (expanding an iso column-word matrix)
 __global__ void k_cw_fill_iso(uint8_t *v, int64_t count, const uint8_t *one, int vsize) {
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < count; e += (int64_t)gridDim.x * blockDim.x)
@@ -828,3 +852,50 @@ bool gb_colbits_assign_scalar(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, const vo
     C->hint_valid = false;
     return true;
 }
+
+// ================================================================== device access (frontier exchange)
+extern "C" {
+
+GrB_Info GxB_Matrix_colwords_view(uint64_t **words, GrB_Index *nwords, GrB_Matrix A) {
+    if (!words || !nwords) return GrB_NULL_POINTER;
+    return gb_api(OBJ(A), [&] {
+        GB_Obj *o = gb_obj_check_raw(A);
+        GB_REQUIRE(small_rows(o), GrB_INVALID_VALUE, "column words need a matrix of 1 to 64 rows");
+        if (!o->cw) to_cw(o, nullptr, 0, nullptr);
+        *words = o->cw;
+        *nwords = (GrB_Index)o->ncols;
+    });
+}
+
+GrB_Info GxB_Matrix_colwords_touch(GrB_Matrix A) {
+    return gb_api(OBJ(A), [&] {
+        GB_Obj *o = gb_obj_check_raw(A);
+        GB_REQUIRE(o->cw, GrB_INVALID_OBJECT, "matrix is not in column-word format");
+        if (!o->iso) {  // every entry written through the view carries the value 1
+            const int vs = (int)o->type->size;
+            char one[16] = {0};
+            gb_with_type(o->type->code, [&](auto z) {
+                using T = decltype(z);
+                T v = gb_cast<T, bool>(true);
+                memcpy(one, &v, sizeof(T));
+            });
+            void *nv = gb_malloc(vs);
+            gb_copy_h2d(nv, one, vs);
+            gb_free(o->cw_vals);
+            o->cw_vals = nv;
+            o->iso = true;
+        }
+        if (!o->pub) o->pub = gb_host_slot_alloc();
+        const uint64_t seq = gb_next_pub_seq();
+        const int64_t n = o->ncols;
+        hipLaunchKernelGGL(k_cw_recount, dim3(cb_grid(n, 2048)), dim3(CB_BLOCK), 0, gb_stream(), o->cw, n, o->cw + n,
+                           o->cw_stat, grid_state(0), gb_host_slot_device(o->pub), (long long)seq);
+        GB_LAUNCH_CHECK();
+        o->nvals_valid = false;
+        o->hint_valid = false;
+        o->pub_seq = seq;
+        o->pub_epoch = gb_epoch();
+    });
+}
+
+}  // extern "C"

@@ -60,6 +60,7 @@ _SIGS = {
     "GxB_Matrix_rmat": [P, E, E, U, E, U, I, I],
     "GxB_Vector_bitmap_export": [P, P, I], "GxB_Vector_bitmap_import": [P, P, I],
     "GxB_Matrix_import_device": [P, P, I, I, P, P, P, I, ctypes.c_bool],
+    "GxB_Matrix_colwords_view": [P, P, P], "GxB_Matrix_colwords_touch": [P],
 }
 for _t in TYPE_NAMES:
     _T = _CTYPES[_t]

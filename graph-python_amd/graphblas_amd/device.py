@@ -38,3 +38,14 @@ def matrix_view(handle):
     if rc != 0:
         raise RuntimeError(f"GxB_Matrix_device_view failed: {rc}")
     return v
+
+
+def colwords_view(handle):
+    """(device address, count) of a <=64-row matrix's column words (GxB_Matrix_colwords_view);
+    rewrite them in place on the library stream, then GxB_Matrix_colwords_touch."""
+    ptr = ctypes.c_void_p()
+    n = ctypes.c_uint64()
+    rc = lib.GxB_Matrix_colwords_view(ctypes.byref(ptr), ctypes.byref(n), handle)
+    if rc != 0:
+        raise RuntimeError(f"GxB_Matrix_colwords_view failed: {rc}")
+    return ptr.value, n.value

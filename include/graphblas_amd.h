@@ -340,6 +340,16 @@ GrB_Info GxB_Vector_device_touch(GrB_Vector v);
  * from device memory on the library stream (frontier exchange over RCCL).
  * Import makes the vector iso-valued 1 (true) on every set bit. */
 GrB_Info GxB_Vector_bitmap_export(GrB_Vector v, void *dst_device, GrB_Index nwords);
+/* Column-word format of a matrix of at most 64 rows (batched frontiers,
+ * gb_colbits.hip): converts A to it if needed and returns the device address of
+ * its ncols 64-bit words (bit r of word j = entry (r, j)).  The words may be
+ * rewritten in place on the library stream (a frontier all-gather over RCCL),
+ * followed by GxB_Matrix_colwords_touch. */
+GrB_Info GxB_Matrix_colwords_view(uint64_t **words, GrB_Index *nwords, GrB_Matrix A);
+/* Recount a column-word matrix (count + summary, published to the host mailbox)
+ * after its words were rewritten; a non-iso matrix becomes iso-valued 1 (true),
+ * like GxB_Vector_bitmap_import. */
+GrB_Info GxB_Matrix_colwords_touch(GrB_Matrix A);
 GrB_Info GxB_Vector_bitmap_import(GrB_Vector v, const void *src_device, GrB_Index nwords);
 /* Build a pattern R-MAT graph on the device (same generator as the oracle):
  * scale, edge factor, seed; values: 0 = BOOL iso true, 1 = INT64 [1,255],

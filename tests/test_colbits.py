@@ -214,3 +214,34 @@ def test_colbits_roundtrip_and_general_ops(gb):
         assert np.array_equal(np.sort(cc[rr == i].astype(np.int64)), np.sort(cols))
     Q.clear()
     assert Q.nvals == 0
+
+
+def test_colwords_view_touch(gb):
+    """the frontier exchange's device access: words copied from one column-word matrix
+    into another through GxB_Matrix_colwords_view, then GxB_Matrix_colwords_touch.
+    (The copy goes through the HIP runtime the library uses: torch's bundled runtime
+    cannot initialise after it in the same process.)"""
+    import ctypes
+
+    from graphblas_amd import device as gdev
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    n = 5000
+    rng = np.random.default_rng(3)
+    r = rng.integers(0, 5, 900)
+    c = rng.integers(0, n, 900)
+    key = np.unique(r * n + c)
+    Q = gb.Matrix.from_coo(key // n, key % n, True, nrows=5, ncols=n)
+    D = gb.Matrix(bool, 5, n)
+    p1, n1 = gdev.colwords_view(Q._h)
+    p2, n2 = gdev.colwords_view(D._h)
+    assert n1 == n2 == n
+    assert hip.hipDeviceSynchronize() == 0
+    assert hip.hipMemcpy(ctypes.c_void_p(p2), ctypes.c_void_p(p1), ctypes.c_size_t(8 * n), 3) == 0
+    assert hip.hipDeviceSynchronize() == 0
+    assert gb.lib.GxB_Matrix_colwords_touch(D._h) == 0
+    assert D.nvals == key.size
+    rr, cc, vv = D.to_coo()
+    assert np.array_equal(rr.astype(np.int64) * n + cc.astype(np.int64), key) and vv.all()
+    with pytest.raises(Exception):
+        gdev.colwords_view(gb.Matrix(bool, 65, 10)._h)
