@@ -163,6 +163,9 @@ def config3_msbfs(lib, torch, stream, O, args, A, n, ap, ai, deg, roots16):
             ok(lib.GrB_mxm(Q, V, None, sr, Q, A, desc), "Q<!V.S> = Q lor.land A")
             ok(lib.GrB_Matrix_nvals(ctypes.byref(nv), Q), "nvals")
             if nv.value == 0:
+                # the level stamps are pending work on V's column words: materialise its
+                # values inside the timed batch
+                ok(lib.GrB_Matrix_wait(V, lib.GrB_MATERIALIZE), "wait V")
                 return d
 
     levels = batch()
@@ -265,6 +268,7 @@ def config3_msbfs_sharded(lib, torch, stream, O, args, dist, world, rank, AT, pa
             exchange()
             ok(lib.GrB_Matrix_nvals(ctypes.byref(nv), Q), "nvals")
             if nv.value == 0:
+                ok(lib.GrB_Matrix_wait(Vl, lib.GrB_MATERIALIZE), "wait Vloc")
                 return d
 
     levels = batch()

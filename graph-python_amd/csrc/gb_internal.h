@@ -251,6 +251,7 @@ GB_Obj *gb_obj_check_raw(const void *p, bool allow_null = false);  // any intern
 // column-word bitmap matrices (gb_colbits.hip)
 void gb_cw_to_csr(GB_Obj *A);    // back to CSR (device work; reads the count)
 void gb_cw_release(GB_Obj *A);   // drop the column-word storage without converting
+void gb_cw_materialize(GB_Obj *A);  // carry out pending level-stamp layers (values)
 GB_Obj *gb_new_object(int kind, GrB_Type type, int64_t nrows, int64_t ncols);
 void gb_obj_free_storage(GB_Obj *A);
 void gb_drop_transpose(GB_Obj *A);

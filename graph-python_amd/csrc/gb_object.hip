@@ -1149,7 +1149,7 @@ GrB_Info GrB_Matrix_free(GrB_Matrix *A) {
 GrB_Info GrB_Matrix_wait(GrB_Matrix A, GrB_WaitMode mode) {
     (void)mode;
     return gb_api(OBJ(A), [&] {
-        gb_obj_check_raw(A);
+        gb_cw_materialize(gb_obj_check_raw(A));  // pending column-word value layers
         gb_sync();
     });
 }

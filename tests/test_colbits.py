@@ -63,7 +63,8 @@ def _msbfs(gb, A, roots, n):
 @pytest.mark.parametrize("direction", [0, 1, 2])  # auto (device-chosen), pull only, push only
 @pytest.mark.parametrize("hub", [0, 8])  # hub pieces of the default 512 edges, or of 8 (most rows)
 @pytest.mark.parametrize("sliced", [0, 1, 3])  # pull XCD-sliced: never (default) / always / when the host knows it pulls
-def test_msbfs_rmat_vs_oracle(gb, scale, k, direction, hub, sliced):
+@pytest.mark.parametrize("eager", [0, 1])  # level stamps as pending layers (default) or written at once
+def test_msbfs_rmat_vs_oracle(gb, scale, k, direction, hub, sliced, eager):
     G = O.rmat(scale, 16, 42)
     n = G.nrows
     r, c, _ = G.to_coo()
@@ -72,7 +73,8 @@ def test_msbfs_rmat_vs_oracle(gb, scale, k, direction, hub, sliced):
     deg = np.diff(G.indptr)
     roots = rng.choice(np.flatnonzero(deg > 0), k, replace=False)
     roots[0] = int(np.argmax(deg))  # the hub: long columns go to the wave path
-    with _knobs(gb, colbits=1, colbits_direction=direction, colbits_hub=hub, colbits_sliced=sliced):
+    with _knobs(gb, colbits=1, colbits_direction=direction, colbits_hub=hub, colbits_sliced=sliced,
+                colbits_eager=eager):
         got, _ = _msbfs(gb, A, roots, n)
     for i, src in enumerate(roots):
         lev, _, _ = O.bfs_levels(G, int(src))
@@ -245,3 +247,33 @@ def test_colwords_view_touch(gb):
     assert np.array_equal(rr.astype(np.int64) * n + cc.astype(np.int64), key) and vv.all()
     with pytest.raises(Exception):
         gdev.colwords_view(gb.Matrix(bool, 65, 10)._h)
+
+
+def test_pending_stamps_wait_and_overwrite(gb):
+    """layers applied in order (a later stamp overwrites an earlier one), across an explicit
+    wait, with more stamps than the layer cap, and through dup / extract"""
+    k, n = 6, 4200
+    rng = np.random.default_rng(11)
+    C = gb.Matrix(gb.INT64, k, n)
+    exp = np.zeros((k, n), np.int64)
+    have = np.zeros((k, n), bool)
+    for step in range(40):  # > CB_MAX_LAYERS (16): materialised on the way
+        r = rng.integers(0, k, 300)
+        c = rng.integers(0, n, 300)
+        key = np.unique(r * n + c)
+        M = gb.Matrix.from_coo(key // n, key % n, True, nrows=k, ncols=n)
+        C(M.S)[:, :] = step + 1
+        exp[key // n, key % n] = step + 1
+        have[key // n, key % n] = True
+        if step == 10:
+            C.wait()
+        if step == 20:
+            D = C.dup()
+            dr, dc, dv = D.to_coo()
+            er, ec = np.nonzero(have)
+            assert np.array_equal(dv, exp[er, ec])
+    assert C.nvals == int(have.sum())
+    gr, gc, gv = C.to_coo()
+    er, ec = np.nonzero(have)
+    assert np.array_equal(gr.astype(np.int64), er) and np.array_equal(gc.astype(np.int64), ec)
+    assert np.array_equal(gv, exp[er, ec])
