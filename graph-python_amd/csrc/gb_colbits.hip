@@ -53,14 +53,6 @@ GB_DEV uint64_t cb_wave_or(uint64_t v) {
     for (int off = 32; off > 0; off >>= 1) v |= cb_shfl(v, (int)(threadIdx.x & 63) ^ off);
     return v;
 }
-GB_DEV bool cb_nonzero(const void *p, int size) {
-    switch (size) {
-        case 1: return *(const uint8_t *)p != 0;
-        case 2: return *(const uint16_t *)p != 0;
-        case 4: return *(const uint32_t *)p != 0;
-        default: return *(const uint64_t *)p != 0;
-    }
-}
 GB_DEV void cb_copy(void *dst, const void *src, int size) {
     switch (size) {
         case 1: *(uint8_t *)dst = *(const uint8_t *)src; break;
@@ -86,7 +78,7 @@ struct cb_step_args {
     const int32_t *sci;
     const uint64_t *M;                      // mask words [nout] (nullptr: no mask)
     const void *m_iso;                      // value mask of an iso matrix: its value (nullptr: structure)
-    int m_iso_size;
+    int m_iso_code;                         // its type (mask truth: -0.0 is false, NaN true)
     bool comp;
     uint64_t full;                          // the k row bits
     uint64_t *out;                          // [nout], zeroed
@@ -212,7 +204,7 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cw_step(cb_step_args a) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    const bool m_on = !a.m_iso || cb_nonzero(a.m_iso, a.m_iso_size);
+    const bool m_on = !a.m_iso || gb_dyn_nonzero(a.m_iso, a.m_iso_code);
     const bool push = a.srp && (a.dir == 2 || (a.dir == 0 && a.stat_in[1] * a.alpha < a.nnz));
     // sparse frontier: test the summary bit (L2-resident) before gathering a word
     const bool use_sum = a.S_in && a.stat_in[2] == 1 && a.stat_in[0] * 4 < a.nin;
@@ -357,7 +349,7 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cw_pull_sl(cb_step_args a, const i
     const int c = blockIdx.x % 8;
     const int64_t wave = (int64_t)(blockIdx.x / 8) * (CB_BLOCK / 64) + wid;
     const int64_t nwaves = (int64_t)(gridDim.x / 8) * (CB_BLOCK / 64);
-    const bool m_on = !a.m_iso || cb_nonzero(a.m_iso, a.m_iso_size);
+    const bool m_on = !a.m_iso || gb_dyn_nonzero(a.m_iso, a.m_iso_code);
     const bool use_sum = a.S_in && a.stat_in[2] == 1 && a.stat_in[0] * 4 < a.nin;
     const int32_t *rp = srp + (int64_t)c * (a.nout + 1);
     const int32_t *ci = scol + sbase[c];
@@ -462,14 +454,14 @@ __global__ void k_cw_fill(const uint64_t *__restrict__ cw, int64_t n, int k, con
 // column with new bits go out as one wave-wide store (lane r -> row r), so a
 // column's values are written as one coalesced segment.
 __global__ __launch_bounds__(CB_BLOCK) void k_cw_assign(int64_t n, int k, const uint64_t *__restrict__ M,
-                                                         const void *m_iso, int m_iso_size, const uint8_t *m_vals,
+                                                         const void *m_iso, int m_code, const uint8_t *m_vals,
                                                          int m_vsize, uint64_t *__restrict__ C, uint8_t *cv,
                                                          unsigned long long x, int vsize, int64_t *stat,
                                                          unsigned long long *gst) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    const bool m_on = !m_iso || cb_nonzero(m_iso, m_iso_size);
+    const bool m_on = !m_iso || gb_dyn_nonzero(m_iso, m_code);
     long long delta = 0;
     for (int64_t base = wave * 64; base < n; base += nwaves * 64) {
         const int64_t j = base + lane;
@@ -479,7 +471,7 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cw_assign(int64_t n, int k, const 
             while (t) {
                 const int r = __ffsll((unsigned long long)t) - 1;
                 t &= t - 1;
-                if (cb_nonzero(m_vals + (j * k + r) * m_vsize, m_vsize)) keep |= 1ULL << r;
+                if (gb_dyn_nonzero(m_vals + (j * k + r) * m_vsize, m_code)) keep |= 1ULL << r;
             }
             m = keep;
         }
@@ -531,10 +523,10 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cw_recount(const uint64_t *__restr
 // nonblocking pending work.  One pass over all entries replaces one scattered store
 // per level (measured: 0.20-0.24 ms per dense level of the 64-root s22 BFS).
 __global__ __launch_bounds__(CB_BLOCK) void k_cw_assign_layer(int64_t n, const uint64_t *__restrict__ M,
-                                                               const void *m_iso, int m_iso_size,
+                                                               const void *m_iso, int m_code,
                                                                uint64_t *__restrict__ C, uint64_t *__restrict__ L,
                                                                int64_t *stat, unsigned long long *gst) {
-    const bool m_on = !m_iso || cb_nonzero(m_iso, m_iso_size);
+    const bool m_on = !m_iso || gb_dyn_nonzero(m_iso, m_code);
     long long delta = 0;
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t m = m_on ? M[j] : 0ULL;
@@ -849,7 +841,7 @@ bool gb_colbits_mxm(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, GrB_Semiring sr, G
     a.sci = dir == 1 ? nullptr : sv.colidx;
     a.M = M ? M->cw : nullptr;
     a.m_iso = (M && !d.structure && M->iso) ? M->cw_vals : nullptr;
-    a.m_iso_size = M ? (int)M->type->size : 1;
+    a.m_iso_code = M ? M->type->code : GBAMD_T_BOOL;
     a.comp = d.comp;
     a.full = k == 64 ? ~0ULL : ((1ULL << k) - 1);
     a.out = out;
@@ -970,7 +962,7 @@ bool gb_colbits_assign_scalar(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, const vo
         gb_cw_materialize(M);
         gb_cw_materialize(C);
         hipLaunchKernelGGL(k_cw_assign, dim3(cb_grid(n, 2048)), dim3(CB_BLOCK), 0, gb_stream(), n, (int)k, M->cw,
-                           nullptr, (int)M->type->size, (const uint8_t *)M->cw_vals, (int)M->type->size, C->cw,
+                           nullptr, M->type->code, (const uint8_t *)M->cw_vals, (int)M->type->size, C->cw,
                            (uint8_t *)C->cw_vals, xv, vs, C->cw_stat, grid_state(0));
         GB_LAUNCH_CHECK();
     } else {
@@ -987,7 +979,7 @@ bool gb_colbits_assign_scalar(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, const vo
         const bool base_empty = nl == 0 && C->nvals_valid && C->nvals == 0;
         uint64_t *L = gb_malloc_n<uint64_t>(n > 0 ? n : 1);
         hipLaunchKernelGGL(k_cw_assign_layer, dim3(cb_grid(n, 2048)), dim3(CB_BLOCK), 0, gb_stream(), n, M->cw, m_iso,
-                           (int)M->type->size, C->cw, L, C->cw_stat, grid_state(0));
+                           M->type->code, C->cw, L, C->cw_stat, grid_state(0));
         GB_LAUNCH_CHECK();
         {
             std::lock_guard<std::mutex> lk(g_layers_mu);

@@ -277,3 +277,17 @@ def test_pending_stamps_wait_and_overwrite(gb):
     er, ec = np.nonzero(have)
     assert np.array_equal(gr.astype(np.int64), er) and np.array_equal(gc.astype(np.int64), ec)
     assert np.array_equal(gv, exp[er, ec])
+
+
+def test_colbits_fp_value_mask_negative_zero(gb):
+    """value masks follow the mask truth of their type: -0.0 is false, NaN true"""
+    k, n = 3, 5000
+    vals = np.array([-0.0, 0.0, np.nan, 2.5, -1.0])
+    rows = np.array([0, 0, 1, 2, 2])
+    cols = np.array([10, 11, 12, 4999, 7])
+    M = gb.Matrix.from_coo(rows, cols, vals, dtype="FP64", nrows=k, ncols=n)
+    C = gb.Matrix(gb.INT32, k, n)
+    C(M.V)[:, :] = 9
+    r, c, v = C.to_coo()
+    got = sorted(zip(r.astype(int).tolist(), c.astype(int).tolist()))
+    assert got == [(1, 12), (2, 7), (2, 4999)] and (v == 9).all()
