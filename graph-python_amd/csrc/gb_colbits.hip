@@ -12,19 +12,22 @@
 // column j (bit r = entry (r, j)), values column-major (cw_vals[j * k + r]).
 // Then one level is one pass over the graph for all k sources:
 //   pull (rows of B^T = in-edges of output column j):  out[j] = OR_i F[i] & need(j),
-//        need(j) = the mask's complement in column j; a lane walks its column's
-//        first CAP edges alone (4 gathers in flight), stops as soon as every needed
-//        bit is found, and hands longer columns to the whole wave (256 edges a
-//        step, wave OR-reduction, same early exit);
+//        need(j) = the mask's complement in column j; a wave owns 64 consecutive
+//        columns and walks their in-edges as one flat list (cb_pull_chunk), columns
+//        longer than 512 edges run as pieces from the cached hub table (a wave per
+//        piece, early exit once every needed bit is found);
 //   push (rows of B = out-edges of frontier column i):  atomicOr(out[j], F[i] & need(j))
 //        with a pre-check, newly set bits counted from the atomic's old value.
 // Direction is chosen on the device (Beamer): push iff the frontier's out-edges x
 // alpha < nnz(B); each level's kernel leaves the next level's edge count
-// (cw_stat[1]) and the count (cw_stat[0], published to the host mailbox).
+// (cw_stat[1]) and the count (cw_stat[0]), both published to the host mailbox.
 // Result values: a boolean LOR/ANY fold of iso operands is iso, its value
 // mult(a, b) computed on the device, so structure is all the kernel produces.
-// Bytes per level (pull): 4 B per scanned edge + 8 B gather per scanned edge
-// (F is n x 8 B = 32 MB at s22: MALL-resident) + 8 B mask + 8 B output per column.
+// Traffic per pull level: 4 B per scanned edge (coalesced) plus one random 8-byte
+// access per scanned edge (the summary bit, or the frontier word F[i]: n x 8 B =
+// 32 MB at s22), each costing a cache line -- that random-line rate, not HBM
+// streaming, bounds the kernel.  Level stamps are pending layers
+// applied when V's values are read.
 //
 // Every other API entry point sees CSR: gb_obj_check converts back (gb_cw_to_csr:
 // per-column popcounts, scan, CSC fill, transpose).
