@@ -828,6 +828,9 @@ bool gb_colbits_mxm(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, GrB_Semiring sr, G
     if (inner != br || C->nrows != k || C->ncols != bc) return false;  // the general path reports it
     // result values: every product's value is mult(a, b) of the iso operand values
     if ((uses_a && !(A->iso || (!A->cw && A->nvals == 0))) || (uses_b && !(B->iso || B->nvals == 0))) return false;
+    // ~NULL selects nothing (C kept, or cleared under replace): the general path's rule
+    // (gb_writeback.hip, gb_make_mmask) -- not a shape of this kernel
+    if (!M && d.comp) return false;
     if (M) {
         if (!small_rows(M) || M->nrows != k || M->ncols != bc) return false;
         if (!d.structure && !M->iso && !(M->cw == nullptr && M->nvals == 0)) return false;

@@ -327,12 +327,22 @@ gb_desc gb_read_desc(const GrB_Descriptor d) {
 
 extern "C" {
 
+static int32_t g_mode = GrB_NONBLOCKING;
+
 GrB_Info GrB_init(GrB_Mode mode) {
-    (void)mode;
     return gb_api(nullptr, [&] {
         GB_REQUIRE(!g_init, GrB_INVALID_VALUE, "GrB_init called twice");
+        GB_REQUIRE(mode == GrB_BLOCKING || mode == GrB_NONBLOCKING, GrB_INVALID_VALUE, "invalid mode");
         gb_do_init();
+        g_mode = mode;
     });
+}
+
+GrB_Info GxB_Global_Option_get_INT32(GxB_Option_Field field, int32_t *value) {
+    if (!value) return GrB_NULL_POINTER;
+    if (field != GxB_MODE) return GrB_INVALID_VALUE;
+    *value = g_mode;
+    return GrB_SUCCESS;
 }
 
 GrB_Info GrB_finalize(void) {

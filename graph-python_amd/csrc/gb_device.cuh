@@ -220,6 +220,16 @@ GB_HD T gb_binop(int op, T x, T y) {
             case GBAMD_OP_BXNOR: return (T)(U)~((U)x ^ (U)y);
             default: break;
             }
+        } else {
+            switch (op) {
+            case GBAMD_OP_ATAN2: return (T)atan2((double)x, (double)y);
+            case GBAMD_OP_HYPOT: return (T)hypot((double)x, (double)y);
+            case GBAMD_OP_FMOD: return (T)fmod((double)x, (double)y);
+            case GBAMD_OP_REMAINDER: return (T)remainder((double)x, (double)y);
+            case GBAMD_OP_LDEXP: return (T)ldexp((double)x, (int)y);
+            case GBAMD_OP_COPYSIGN: return (T)copysign((double)x, (double)y);
+            default: break;
+            }
         }
         return zero;
     }

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "../../include/gbamd_codes.h"
 #include "gb_state.h"
@@ -253,6 +254,7 @@ void gb_cw_to_csr(GB_Obj *A);    // back to CSR (device work; reads the count)
 void gb_cw_release(GB_Obj *A);   // drop the column-word storage without converting
 void gb_cw_materialize(GB_Obj *A);  // carry out pending level-stamp layers (values)
 GB_Obj *gb_new_object(int kind, GrB_Type type, int64_t nrows, int64_t ncols);
+extern "C" void gb_vec_recount(GB_Obj *v);  // a vector's bitmap changed on the device: recount + publish
 void gb_obj_free_storage(GB_Obj *A);
 void gb_drop_transpose(GB_Obj *A);
 int64_t gb_nvals(GB_Obj *A);           // exact (may synchronise for bitmaps)
@@ -343,6 +345,16 @@ void *gb_expand_iso(const void *one_value, size_t tsize, int64_t n);
 void gb_transpose_csr(int64_t nrows, int64_t ncols, int64_t nvals, const int64_t *rowptr,
                       const int32_t *colidx, const void *vals, size_t tsize, bool iso,
                       int64_t **trowptr, int32_t **tcolidx, void **tvals, int64_t **tperm = nullptr);
+
+// ------------------------------------------------------------------ index lists
+// GrB_ALL, an explicit list, or the GxB_RANGE / GxB_STRIDE / GxB_BACKWARDS encodings
+// (gb_extract.hip), expanded on the host and checked against n
+struct gb_index_list {
+    bool all = false;          // GrB_ALL: idx is empty, the list is 0 .. n-1
+    int64_t n = 0;             // length of the list
+    std::vector<int64_t> idx;  // explicit indices (all == false)
+};
+void gb_expand_indices(gb_index_list &L, const GrB_Index *I, GrB_Index ni, int64_t n);
 
 // ------------------------------------------------------------------ ops
 struct gb_desc {

@@ -290,7 +290,7 @@ void gb_get_csc(gb_csr_view &v, GB_Obj *A) {
     if (A->kind == GB_KIND_MATRIX) {
         if (!A->t_valid) {
             gb_transpose_csr(A->nrows, A->ncols, A->nvals, A->rowptr, A->colidx, A->vals,
-                             A->type->size, A->iso, &A->t_rowptr, &A->t_colidx, &A->t_vals, &A->t_perm);
+                             A->type->size, A->iso, &A->t_rowptr, &A->t_colidx, &A->t_vals);
             A->t_valid = true;
         }
         v.nrows = A->ncols;
@@ -321,10 +321,42 @@ void gb_get_csc(gb_csr_view &v, GB_Obj *A) {
     v.iso = c.iso;
 }
 
+// perm[q] = CSR position of the CSC entry q: a wave per CSC row j, each lane binary-searches
+// column j in the CSR row of its entry (built on first use; only the two-sided masked dot
+// reads it, for a matrix used as a structural mask)
+__global__ __launch_bounds__(256) void k_csc_perm(int64_t ncols, const int64_t *__restrict__ trp,
+                                                  const int32_t *__restrict__ tci, const int64_t *__restrict__ rp,
+                                                  const int32_t *__restrict__ ci, int64_t *__restrict__ perm) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t j = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; j < ncols; j += nwaves) {
+        for (int64_t q = trp[j] + lane; q < trp[j + 1]; q += 64) {
+            const int64_t i = tci[q];
+            int64_t lo = rp[i], hi = rp[i + 1];
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (ci[mid] < j) lo = mid + 1;
+                else hi = mid;
+            }
+            perm[q] = lo;
+        }
+    }
+}
+
 const int64_t *gb_csc_perm(GB_Obj *A) {
     GB_REQUIRE(A->kind == GB_KIND_MATRIX, GrB_INVALID_VALUE, "CSC position map of a non-matrix");
     gb_csr_view v;
     gb_get_csc(v, A);
+    if (!A->t_perm) {
+        A->t_perm = gb_malloc_n<int64_t>(A->nvals ? A->nvals : 1);
+        if (A->nvals) {
+            int64_t blocks = (A->ncols + 3) / 4;
+            if (blocks > 65535) blocks = 65535;
+            hipLaunchKernelGGL(k_csc_perm, dim3((unsigned)blocks), dim3(256), 0, gb_stream(), A->ncols, A->t_rowptr,
+                               A->t_colidx, A->rowptr, A->colidx, A->t_perm);
+            GB_LAUNCH_CHECK();
+        }
+    }
     return A->t_perm;
 }
 
@@ -1434,6 +1466,7 @@ static void vec_recount_published(GB_Obj *o) {
     o->pub_seq = seq;
     o->pub_epoch = gb_epoch();
 }
+void gb_vec_recount(GB_Obj *o) { vec_recount_published(o); }
 GrB_Info GxB_Vector_device_touch(GrB_Vector v) {
     return gb_api(OBJ(v), [&] {
         GB_Obj *o = gb_obj_check(v);

@@ -432,10 +432,11 @@ static void scalar_vec_T(gb_vec_result &T, int64_t n, const GrB_Index *I, int64_
     }
     std::vector<uint64_t> hb(nw, 0);
     int64_t c = 0;
-    for (int64_t q = 0; q < ni; q++) {
-        GB_REQUIRE(I[q] < (GrB_Index)n, GrB_INDEX_OUT_OF_BOUNDS, "assign index out of bounds");
-        uint64_t &w = hb[I[q] >> 6];
-        uint64_t b = 1ULL << (I[q] & 63);
+    gb_index_list L;
+    gb_expand_indices(L, I, (GrB_Index)ni, n);
+    for (int64_t i : L.idx) {
+        uint64_t &w = hb[i >> 6];
+        uint64_t b = 1ULL << (i & 63);
         if (!(w & b)) c++;
         w |= b;
     }
@@ -705,21 +706,22 @@ static void matrix_assign_scalar(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, const
         });
     });
     int64_t nr = C->nrows, nc = ncols_of(C);
-    std::vector<GrB_Index> rows, cols;
-    if (I == GrB_ALL) {
+    gb_index_list LI, LJ;
+    gb_expand_indices(LI, I, (GrB_Index)ni, nr);
+    gb_expand_indices(LJ, J, (GrB_Index)nj, nc);
+    std::vector<int64_t> rows, cols;
+    if (LI.all) {
         rows.resize(nr);
         for (int64_t i = 0; i < nr; i++) rows[i] = i;
-    } else rows.assign(I, I + ni);
-    if (J == GrB_ALL) {
+    } else rows = LI.idx;
+    if (LJ.all) {
         cols.resize(nc);
         for (int64_t j = 0; j < nc; j++) cols[j] = j;
-    } else cols.assign(J, J + nj);
+    } else cols = LJ.idx;
     std::sort(rows.begin(), rows.end());
     rows.erase(std::unique(rows.begin(), rows.end()), rows.end());
     std::sort(cols.begin(), cols.end());
     cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
-    for (auto r : rows) GB_REQUIRE(r < (GrB_Index)nr, GrB_INDEX_OUT_OF_BOUNDS, "row index out of bounds");
-    for (auto c : cols) GB_REQUIRE(c < (GrB_Index)nc, GrB_INDEX_OUT_OF_BOUNDS, "column index out of bounds");
     int64_t nz = (int64_t)rows.size() * (int64_t)cols.size();
     std::vector<int64_t> rp(nr + 1, 0);
     for (auto r : rows) rp[r + 1] = (int64_t)cols.size();
@@ -979,6 +981,34 @@ GrB_Info GrB_transpose(GrB_Matrix C, const GrB_Matrix Mask, const GrB_BinaryOp a
     });
 }
 
+// w(I) = u without accum replaces the region: entries of w at I (where the mask selects)
+// that u does not hold are deleted.  Clears those bits before the merge with accum SECOND.
+__global__ void k_clear_region(int64_t nw, uint64_t *__restrict__ wbits, const uint64_t *__restrict__ rbits,
+                               const uint64_t *__restrict__ mbits, bool mcomp) {
+    OPS_STRIDE(k, nw) {
+        uint64_t sel = mbits ? (mcomp ? ~mbits[k] : mbits[k]) : ~0ULL;
+        wbits[k] &= ~(rbits[k] & sel);
+    }
+}
+
+static void vector_clear_region(GB_Obj *W, const gb_index_list &L, GB_Obj *M, const gb_desc &d) {
+    const int64_t n = W->nrows, nw = gb_words(n);
+    GB_REQUIRE(W->kind != GB_KIND_MATRIX, GrB_NOT_IMPLEMENTED, "index-list assign into an n x 1 matrix");
+    if (nw == 0) return;
+    std::vector<uint64_t> hr(nw, 0);
+    for (int64_t i : L.idx) hr[i >> 6] |= 1ULL << (i & 63);
+    gb_scratch s;
+    uint64_t *r = s.get<uint64_t>(nw);
+    gb_copy_h2d(r, hr.data(), nw * sizeof(uint64_t));
+    gb_vmask m;
+    gb_make_vmask(m, M, d, n);
+    hipLaunchKernelGGL(k_clear_region, dim3(ops_grid(nw)), dim3(OPS_BLOCK), 0, gb_stream(), nw, W->bits, r, m.bits,
+                       m.comp);
+    GB_LAUNCH_CHECK();
+    gb_vec_recount(W);
+    gb_sync();
+}
+
 GrB_Info GrB_Vector_assign(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum, const GrB_Vector u,
                            const GrB_Index *I, GrB_Index ni, const GrB_Descriptor desc) {
     return gb_api(OBJ(w), [&] {
@@ -1005,7 +1035,9 @@ GrB_Info GrB_Vector_assign(GrB_Vector w, const GrB_Vector mask, const GrB_Binary
             return;
         }
         // index list: w(I[k]) = u(k)
-        GB_REQUIRE((GrB_Index)U->nrows == ni, GrB_DIMENSION_MISMATCH, "u size does not match the index list");
+        gb_index_list L;
+        gb_expand_indices(L, I, ni, n);
+        GB_REQUIRE(U->nrows == L.n, GrB_DIMENSION_MISMATCH, "u size does not match the index list");
         int64_t unv = gb_nvals(U);
         std::vector<GrB_Index> ui(unv);
         std::vector<char> ux(unv * U->type->size);
@@ -1016,8 +1048,8 @@ GrB_Info GrB_Vector_assign(GrB_Vector w, const GrB_Vector mask, const GrB_Binary
         GB_Obj *Tv = gb_new_object(GB_KIND_VECTOR, U->type, n, 1);
         std::vector<GrB_Index> wi(unv);
         for (int64_t q = 0; q < unv; q++) {
-            GB_REQUIRE(ui[q] < ni && I[ui[q]] < (GrB_Index)n, GrB_INDEX_OUT_OF_BOUNDS, "index out of bounds");
-            wi[q] = I[ui[q]];
+            GB_REQUIRE(ui[q] < (GrB_Index)L.n, GrB_INDEX_OUT_OF_BOUNDS, "index out of bounds");
+            wi[q] = (GrB_Index)L.idx[ui[q]];
         }
         try {
             gb_build(Tv, wi.data(), nullptr, ux.data(), U->type->code, false, unv, nullptr);
@@ -1038,6 +1070,7 @@ GrB_Info GrB_Vector_assign(GrB_Vector w, const GrB_Vector mask, const GrB_Binary
         gb_bitmap_count(T.bits, n, T.d_nvals);
         GrB_Vector tv = (GrB_Vector)Tv;
         GrB_Vector_free(&tv);
+        if (!accum) vector_clear_region(W, L, gb_obj_check(mask, true), d);
         gb_writeback_vector(W, T, gb_obj_check(mask, true), d, accum ? accum : second_of(W->type->code), false);
     });
 }

@@ -55,6 +55,8 @@ _SIGS = {
     "GrB_Matrix_reduce_Monoid": [P] * 6, "GrB_Matrix_reduce_BinaryOp": [P] * 6,
     "GrB_Vector_apply": [P] * 6, "GrB_Matrix_apply": [P] * 6,
     "GrB_Semiring_new": [P, P, P], "GrB_UnaryOp_free": [P],
+    "GrB_Matrix_extract": [P, P, P, P, P, I, P, I, P], "GrB_Col_extract": [P, P, P, P, P, I, I, P],
+    "GrB_Vector_extract": [P, P, P, P, P, I, P], "GxB_Global_Option_get_INT32": [E, P],
     "GxB_Matrix_device_view": [P, P], "GxB_Vector_device_view": [P, P],
     "GxB_Vector_device_touch": [P], "GxB_Matrix_prepare_transpose": [P],
     "GxB_Matrix_rmat": [P, E, E, U, E, U, I, I],

@@ -203,6 +203,55 @@ class Mask:
     def name(self):
         return self.parent.name
 
+    def __eq__(self, other):
+        raise TypeError(f"__eq__ not defined for objects of type {type(self)}.")
+
+    def __bool__(self):
+        raise TypeError(f"__bool__ not defined for objects of type {type(self)}.")
+
+    __hash__ = object.__hash__
+
+    # ---- mask algebra (reference core/mask.py:34-128).  The reference picks one of 16
+    # recipes per (mask kind, mask kind) pair; each recipe computes the set its docstring
+    # defines, and that definition is what is issued here -- masked assigns on the device:
+    #   new(mask=m2)                 val(m1) << True; val(m2, replace=True) << val   (:51-56)
+    #   new(mask=m2, complement=True) val(~m1) << True; val(~m2) << True             (:58-63)
+    #   m1 & m2                      the set of new(mask=m2) as a structural mask    (:86-91)
+    #   m1 | m2                      val(m1) << True; val(m2) << True; val.S          (:114-118)
+    def new(self, dtype=None, *, complement=False, mask=None, name=None, **opts):
+        if dtype is None:
+            dtype = BOOL
+        val = type(self.parent)(dtype, *self.parent.shape, name=name)
+        if mask is None:
+            val(~self if complement else self, **opts) << True
+            return val
+        mask = _check_mask(mask)
+        if complement:
+            val(~self, **opts) << True
+            val(~mask, **opts) << True
+        else:
+            val(self, **opts) << True
+            val(mask, replace=True, **opts) << val
+        return val
+
+    def __and__(self, other, **opts):
+        other = _check_mask(other)
+        complement = self.complement or other.complement
+        val = self.new(BOOL, mask=other, complement=complement, **opts)
+        # with a complemented operand the complement of the intersection is the smaller object
+        return ComplementedStructuralMask(val) if complement else StructuralMask(val)
+
+    __rand__ = __and__
+
+    def __or__(self, other, **opts):
+        other = _check_mask(other)
+        val = type(self.parent)(BOOL, *self.parent.shape)
+        val(self, **opts) << True
+        val(other, **opts) << True
+        return StructuralMask(val)
+
+    __ror__ = __or__
+
 
 class StructuralMask(Mask):
     complement, structure = False, True
@@ -253,6 +302,7 @@ class _ReplaceSentinel:
 
 
 replace = _ReplaceSentinel()
+_REPLACE = replace  # BaseType.__call__'s `replace` parameter shadows the module name
 
 
 def _normalize_accum(accum, dtype):
@@ -262,7 +312,8 @@ def _normalize_accum(accum, dtype):
     if accum.opclass == "Monoid":
         accum = getattr(binary, accum.parent.name if accum.parent.name != "eq" else "lxnor")[accum.type]
     elif accum.opclass != "BinaryOp":
-        raise TypeError(f"accum must be a BinaryOp or Monoid, got {accum.opclass}")
+        # reference core/base.py:256 -> _expect_op: "Expected type: BinaryOp, Monoid ..."
+        raise TypeError(f"Expected type: BinaryOp, Monoid for accum; got {accum.opclass}")
     return accum
 
 
@@ -318,7 +369,7 @@ class BaseType:
         """reference core/base.py:192-263"""
         mask_arg = accum_arg = None
         for arg in optional_mask_accum_replace:
-            if arg is replace:
+            if arg is _REPLACE:
                 replace = True
             elif isinstance(arg, (BaseType, Mask)):
                 if self._is_scalar:

@@ -64,6 +64,10 @@ def _matmul_infix_expr(left, right):
 
 def _ewise_infix_expr(left, right, method):
     """`x & y` (eWiseMult) / `x | y` (eWiseAdd) (reference core/infix.py:251-259, 388-397)."""
+    from .base import Mask
+
+    if isinstance(right, Mask):  # v | mask, v & mask (reference core/infix.py:420-423)
+        return right.__ror__(left) if method == "ewise_add" else right.__rand__(left)
     if getattr(left, "ndim", None) is None or getattr(right, "ndim", None) is None:
         return NotImplemented
     return InfixExpr(left, right, method)

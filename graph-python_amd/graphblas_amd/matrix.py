@@ -31,6 +31,8 @@ def _values_dtype(values, dtype):
     if dtype is not None:
         return lookup_dtype(dtype)
     a = np.asarray(values)
+    if a.dtype == object:  # reference core/utils.py values_to_numpy_buffer
+        raise ValueError("object dtype for values is not allowed")
     if a.dtype == np.bool_:
         return lookup_dtype(BOOL)
     if np.issubdtype(a.dtype, np.integer) or np.issubdtype(a.dtype, np.floating):
@@ -60,6 +62,8 @@ class Matrix(BaseType):
 
     def __del__(self):
         h = getattr(self, "_h", None)
+        if getattr(self, "_parent", None) is not None:
+            return  # a cast view (Vector._as_matrix) does not own the handle
         if h is not None and h.value:
             try:
                 lib.GrB_Matrix_free(ctypes.byref(h))
@@ -234,8 +238,23 @@ class Matrix(BaseType):
 
     # ---------------------------------------------------------------- elements
     def __getitem__(self, keys):
-        i, j = _scalar_keys(keys, 2)
-        return _MatrixElement(self, i, j)
+        """A[i, j] element; A[I, J] -> GrB_Matrix_extract; A[I, j] / A[i, J] -> GrB_Col_extract
+        (the row form with INP0 transposed), reference core/matrix.py:2860-2920."""
+        if not isinstance(keys, tuple) or len(keys) != 2:
+            raise TypeError("Matrix indexing requires a (rows, columns) pair")
+        rk, rc, rn = _axis_index(keys[0], self._nrows)
+        ck, cc, cn = _axis_index(keys[1], self._ncols)
+        if rk == "scalar" and ck == "scalar":
+            return _MatrixElement(self, rc, cc)
+        from .vector import VectorExpression
+
+        if rk == "scalar":
+            return VectorExpression("extract", "GrB_Col_extract", [self, cc, cn, rc], at=True, dtype=self.dtype,
+                                    size=cn)
+        if ck == "scalar":
+            return VectorExpression("extract", "GrB_Col_extract", [self, rc, rn, cc], dtype=self.dtype, size=rn)
+        return MatrixExpression("extract", "GrB_Matrix_extract", [self, rc, rn, cc, cn], dtype=self.dtype,
+                                nrows=rn, ncols=cn)
 
     def __setitem__(self, keys, value):
         if keys is Ellipsis or (isinstance(keys, tuple) and all(k == slice(None) for k in keys)):
@@ -261,12 +280,12 @@ class Matrix(BaseType):
         if keys not in (Ellipsis,) and not (isinstance(keys, tuple) and all(k == slice(None) for k in keys)) \
                 and keys != slice(None):
             raise NotImplementedError("Matrix assign supports whole-matrix (A[:, :]) targets")
-        desc = descriptor_lookup(mask_complement=mask.complement if mask else False,
-                                 mask_structure=mask.structure if mask else False,
+        desc = descriptor_lookup(mask_complement=mask.complement if mask is not None else False,
+                                 mask_structure=mask.structure if mask is not None else False,
                                  output_replace=replace)
         if isinstance(value, TransposedMatrix):
-            desc = descriptor_lookup(mask_complement=mask.complement if mask else False,
-                                     mask_structure=mask.structure if mask else False,
+            desc = descriptor_lookup(mask_complement=mask.complement if mask is not None else False,
+                                     mask_structure=mask.structure if mask is not None else False,
                                      output_replace=replace, transpose_first=True)
             value = value._matrix
         if isinstance(value, Matrix):
@@ -359,6 +378,33 @@ def _power(updater, A, n, op):
             break
         base = base.mxm(base, op).new()
     updater << result
+
+
+def _axis_index(key, size):
+    """One axis of an index: ("scalar", i, 1), or ("list", GrB_ALL | _CArray, length).  Slices
+    other than ':' become explicit index arrays (the reference's non-SuiteSparse path,
+    core/slice.py:26-33)."""
+    if isinstance(key, (int, np.integer)) and not isinstance(key, bool):
+        i = int(key)
+        if i < 0:
+            i += size
+        if not 0 <= i < size:
+            raise IndexError(f"index {int(key)} out of range for size {size}")
+        return "scalar", i, 1
+    if isinstance(key, slice):
+        start, stop, step = key.indices(size)
+        n = len(range(start, stop, step))
+        if n == size and step == 1:
+            return "list", lib.GrB_ALL, size
+        return "list", _CArray(np.arange(start, stop, step, dtype=np.uint64), "I"), n
+    arr = np.asarray(key)
+    if arr.dtype == np.bool_:
+        raise TypeError("boolean index arrays are not supported")
+    arr = np.where(arr < 0, arr + size, arr) if arr.size else arr
+    arr = _index_array(np.atleast_1d(arr), "indices")
+    if arr.size and int(arr.max()) >= size:
+        raise IndexError(f"index {int(arr.max())} out of range for size {size}")
+    return "list", _CArray(arr, "I"), int(arr.size)
 
 
 def _scalar_keys(keys, nd):

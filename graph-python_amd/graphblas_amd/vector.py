@@ -12,8 +12,8 @@ from .base import (BaseExpression, BaseType, StructuralMask, ValueMask, _autonam
                    descriptor_lookup)
 from .dtypes import BOOL, FP64, lookup_dtype
 from .exceptions import DimensionMismatch, NoValue, check_status_carg
-from .matrix import Matrix, MatrixExpression, TransposedMatrix, _apply_expr, _binary_for, _CArray, \
-    _index_array, _reduce_scalar, _values_dtype
+from .matrix import Matrix, MatrixExpression, TransposedMatrix, _apply_expr, _axis_index, _binary_for, \
+    _CArray, _index_array, _reduce_scalar, _values_dtype
 
 
 class Vector(BaseType):
@@ -159,9 +159,22 @@ class Vector(BaseType):
 
     # ---------------------------------------------------------------- elements / assign
     def __getitem__(self, key):
-        if isinstance(key, (int, np.integer)) and not isinstance(key, bool):
-            return _VectorElement(self, int(key))
-        raise NotImplementedError("only scalar element indexing is supported for extract")
+        """v[i] element; v[I] -> GrB_Vector_extract (reference core/vector.py:1010-1030)."""
+        kind, idx, n = _axis_index(key, self._size)
+        if kind == "scalar":
+            return _VectorElement(self, idx)
+        return VectorExpression("extract", "GrB_Vector_extract", [self, idx, n], dtype=self.dtype, size=n)
+
+    def _as_matrix(self):
+        """The same object as an n x 1 Matrix (reference core/vector.py:186-205: a
+        `(GrB_Matrix)` cast of the handle; the library accepts either kind)."""
+        A = Matrix.__new__(Matrix)
+        A.dtype = self.dtype
+        A.name = f"(GrB_Matrix){self.name}"
+        A._h = ctypes.c_void_p(self._h.value)
+        A._nrows, A._ncols = self._size, 1
+        A._parent = self
+        return A
 
     def __setitem__(self, key, value):
         if isinstance(key, (int, np.integer)) and not isinstance(key, bool):
@@ -192,8 +205,8 @@ class Vector(BaseType):
             arr = _index_array(np.atleast_1d(keys), "indices")
             idx_obj = _CArray(arr, "I")
             idx, ni = idx_obj, arr.size
-        desc = descriptor_lookup(mask_complement=mask.complement if mask else False,
-                                 mask_structure=mask.structure if mask else False, output_replace=replace)
+        desc = descriptor_lookup(mask_complement=mask.complement if mask is not None else False,
+                                 mask_structure=mask.structure if mask is not None else False, output_replace=replace)
         if isinstance(value, Vector):
             call("GrB_Vector_assign", [self, mask, accum, value, idx, ni, desc])
             return

@@ -15,7 +15,6 @@ Scope: the vanilla C API 2.0 surface of the masked mxm/mxv/vxm path (SURVEY.md
 not provided.  See INTEGRATION.md.
 """
 import os
-import types
 
 import cffi
 
@@ -35,8 +34,41 @@ if not os.path.exists(_SO):
                       "'import __graft_entry__; __graft_entry__.build()')")
 _dl = ffi.dlopen(_SO)
 
-# eager namespace: every declared name resolved once (vars(lib) must list them)
-lib = types.SimpleNamespace(**{name: getattr(_dl, name) for name in dir(_dl)})
+class _GlobalVar:
+    """What `vars(lib)` holds for a C global variable (builtin types, operators, semirings,
+    descriptors, GrB_ALL), as in the compiled cffi module python-graphblas normally gets:
+    not the value and not callable, so the "suitesparse-vanilla" strip
+    (`callable(val) and key.startswith("GxB")`, reference graphblas/__init__.py:180-184)
+    keeps GxB_* objects and drops only GxB_* functions; `getattr(lib, name)` returns the
+    value (the strip copies with getattr, :184)."""
+
+    __slots__ = ("name",)
+
+    def __init__(self, name):
+        self.name = name
+
+    def __repr__(self):
+        return f"<global variable {self.name}>"
+
+
+def _make_lib():
+    """`lib`: every declared function, integer constant and global variable, resolved once
+    (vars(lib) lists them all; reference core/operator/base.py:291 scans dir(lib))."""
+    props, inst = {}, {}
+    for name in dir(_dl):
+        val = getattr(_dl, name)
+        if isinstance(val, ffi.CData) and ffi.typeof(val).kind != "function":
+            props[name] = property(lambda self, _v=val: _v)  # data descriptor: wins over vars()
+            inst[name] = _GlobalVar(name)
+        else:
+            inst[name] = val
+    cls = type("lib", (), props)
+    obj = cls()
+    obj.__dict__.update(inst)
+    return obj
+
+
+lib = _make_lib()
 
 _initialized = False
 

@@ -52,7 +52,20 @@ extern "C" {
 #define GRB_SUBVERSION 0
 
 typedef uint64_t GrB_Index;
+/* index constants as SuiteSparse:GraphBLAS 7.4 defines them (python-graphblas reads them
+ * from lib: GxB_RANGE/GxB_STRIDE/GxB_BACKWARDS in core/slice.py:10-49, and its vanilla
+ * backend deletes GxB_BACKWARDS/GxB_STRIDE from lib, graphblas/__init__.py:185-186) */
 #define GrB_INDEX_MAX ((GrB_Index)(1ULL << 60) - 1)
+#define GxB_INDEX_MAX ((GrB_Index)(1ULL << 60))
+/* special values of ni in assign/extract: I = [begin, end] (RANGE), [begin, end, inc]
+ * (STRIDE), [begin, end, dec] (BACKWARDS), bounds inclusive */
+#define GxB_RANGE (INT64_MAX)
+#define GxB_STRIDE (INT64_MAX - 1)
+#define GxB_BACKWARDS (INT64_MAX - 2)
+#define GxB_BEGIN 0
+#define GxB_END 1
+#define GxB_INC 2
+#define GxB_MAX_NAME_LEN 128
 
 typedef enum {
     GrB_SUCCESS = 0,
@@ -85,6 +98,9 @@ typedef enum {
     GrB_TRAN = 3
 } GrB_Desc_Value;
 typedef enum { GrB_CSR_FORMAT = 0, GrB_CSC_FORMAT = 1, GrB_COO_FORMAT = 2 } GrB_Format;
+/* global option fields (GxB_Global_Option_get_INT32; python-graphblas reads GxB_MODE when the
+ * library was initialised before it, graphblas/__init__.py:156-166) */
+typedef enum { GxB_MODE = 2 } GxB_Option_Field;
 
 typedef struct GB_Type_opaque *GrB_Type;
 typedef struct GB_BinaryOp_opaque *GrB_BinaryOp;
@@ -309,6 +325,22 @@ GrB_Info GrB_Matrix_apply(GrB_Matrix C, const GrB_Matrix Mask, const GrB_BinaryO
                           const GrB_UnaryOp op, const GrB_Matrix A, const GrB_Descriptor desc);
 GrB_Info GrB_transpose(GrB_Matrix C, const GrB_Matrix Mask, const GrB_BinaryOp accum,
                        const GrB_Matrix A, const GrB_Descriptor desc);
+
+/* extract (reference core/matrix.py:2868 "GrB_Matrix_extract", :2903/2917 "GrB_Col_extract",
+ * core/vector.py:1026 "GrB_Vector_extract"): C<M> = accum(C, A'(I, J)); w<m> = accum(w, A'(I, j));
+ * w<m> = accum(w, u(I)).  I, J: GrB_ALL, an explicit list, or the GxB_RANGE / GxB_STRIDE /
+ * GxB_BACKWARDS encodings above. */
+GrB_Info GrB_Matrix_extract(GrB_Matrix C, const GrB_Matrix Mask, const GrB_BinaryOp accum,
+                            const GrB_Matrix A, const GrB_Index *I, GrB_Index ni,
+                            const GrB_Index *J, GrB_Index nj, const GrB_Descriptor desc);
+GrB_Info GrB_Col_extract(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum,
+                         const GrB_Matrix A, const GrB_Index *I, GrB_Index ni, GrB_Index j,
+                         const GrB_Descriptor desc);
+GrB_Info GrB_Vector_extract(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum,
+                            const GrB_Vector u, const GrB_Index *I, GrB_Index ni,
+                            const GrB_Descriptor desc);
+/* GrB_MODE of the running library (GrB_BLOCKING / GrB_NONBLOCKING) for field GxB_MODE */
+GrB_Info GxB_Global_Option_get_INT32(GxB_Option_Field field, int32_t *value);
 
 /* ---------------------------------------------------------------- device extensions */
 /* Zero-copy views of device storage, for RCCL / torch.distributed exchange of

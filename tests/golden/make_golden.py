@@ -341,6 +341,39 @@ def main():
                     c["test_recorder"] = {"expected": _literal(sub.comparators[0]),
                                           "src": f"{tr}:{sub.lineno}"}
 
+    # test_resolving.py: the literal inputs / expected results of the output-binding tests
+    # (dtype resolution, Updater argument order, accumulators, extraction by index lists);
+    # dtype keywords given as names (dtypes.INT32, float) are kept as their source text
+    tres = "graphblas/tests/test_resolving.py"
+    tree = ast.parse(open(os.path.join(REF, tres)).read())
+    fns = {n.name: n for n in ast.walk(tree) if isinstance(n, ast.FunctionDef)}
+    res = {}
+    for fname in ["test_from_coo_dtype_resolving", "test_from_coo_invalid_dtype",
+                  "test_resolve_ops_using_common_dtype", "test_order_of_updater_params_does_not_matter",
+                  "test_already_resolved_ops_allowed_in_updater", "test_updater_returns_updater",
+                  "test_py_indices"]:
+        lst = []
+        for n in ast.walk(fns[fname]):
+            if not (isinstance(n, ast.Call) and isinstance(n.func, ast.Attribute) and n.func.attr == "from_coo"
+                    and isinstance(n.func.value, ast.Name)):
+                continue
+            try:
+                args = [_literal(a) for a in n.args]
+            except ValueError:
+                continue  # data built in the test (np.arange ...): restated in the test itself
+            kw = {}
+            for k in n.keywords:
+                try:
+                    kw[k.arg] = _literal(k.value)
+                except ValueError:
+                    kw[k.arg] = ast.unparse(k.value)
+            d = coo({"kind": n.func.value.id, "args": args, "kw": kw, "src": f"{tres}:{n.lineno}"})
+            d.update(kind=n.func.value.id, dtype=kw.get("dtype"), line=n.lineno)
+            lst.append(d)
+        lst.sort(key=lambda d: d["line"])
+        res[fname] = lst
+    c["test_resolving"] = {"src": tres, "cases": res}
+
     # notebooks (survey-derived expected values, computed independently here)
     data = notebook_graph()
     rows, cols, w = data

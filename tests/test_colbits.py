@@ -41,7 +41,8 @@ def _knobs(gb, **kv):
     return K()
 
 
-def _msbfs(gb, A, roots, n):
+def _msbfs(gb, A, roots, n, semiring="lor_land"):
+    sr = getattr(gb.semiring, semiring)
     k = len(roots)
     Q = gb.Matrix.from_coo(np.arange(k), roots, True, nrows=k, ncols=n)
     V = gb.Matrix(gb.INT32, k, n)
@@ -49,7 +50,7 @@ def _msbfs(gb, A, roots, n):
     while True:
         d += 1
         V(mask=Q.V)[:, :] = d
-        Q(~V.S, replace=True) << Q.mxm(A, gb.semiring.lor_land)
+        Q(~V.S, replace=True) << Q.mxm(A, sr)
         if Q.nvals == 0:
             break
     r, c, x = V.to_coo()
@@ -76,6 +77,28 @@ def test_msbfs_rmat_vs_oracle(gb, scale, k, direction, hub, sliced, eager):
     with _knobs(gb, colbits=1, colbits_direction=direction, colbits_hub=hub, colbits_sliced=sliced,
                 colbits_eager=eager):
         got, _ = _msbfs(gb, A, roots, n)
+    for i, src in enumerate(roots):
+        lev, _, _ = O.bfs_levels(G, int(src))
+        assert np.array_equal(got[i], lev), f"root {src} (row {i})"
+
+
+@pytest.mark.parametrize("scale", [10, 13])
+@pytest.mark.parametrize("k", [1, 7, 64])
+@pytest.mark.parametrize("direction", [0, 1, 2])
+@pytest.mark.parametrize("hub", [0, 8])
+def test_msbfs_any_pair_vs_oracle(gb, scale, k, direction, hub):
+    """BASELINE.json configs[2] names any_pair BOOL: the batched BFS with GxB_ANY_PAIR_BOOL, every
+    direction mode (the ANY monoid + PAIR multiplier take the column-word path, gb_colbits.hip)"""
+    G = O.rmat(scale, 16, 42)
+    n = G.nrows
+    r, c, _ = G.to_coo()
+    A = gb.Matrix.from_coo(r, c, True, nrows=n, ncols=n)
+    rng = np.random.default_rng(scale * 1000 + k)
+    deg = np.diff(G.indptr)
+    roots = rng.choice(np.flatnonzero(deg > 0), k, replace=False)
+    roots[0] = int(np.argmax(deg))
+    with _knobs(gb, colbits=1, colbits_direction=direction, colbits_hub=hub):
+        got, _ = _msbfs(gb, A, roots, n, "any_pair")
     for i, src in enumerate(roots):
         lev, _, _ = O.bfs_levels(G, int(src))
         assert np.array_equal(got[i], lev), f"root {src} (row {i})"
@@ -127,7 +150,8 @@ SR = [("lor_land", "LOR", "LAND"), ("any_pair", "ANY", "PAIR"), ("lor_first", "L
 
 
 @pytest.mark.parametrize("name,mon,mul", SR)
-@pytest.mark.parametrize("masked", ["none", "struct", "comp_replace", "value_iso", "value_replace", "keep"])
+@pytest.mark.parametrize("masked", ["none", "struct", "comp_replace", "value_iso", "value_replace", "keep",
+                                    "nullcomp", "nullcomp_replace"])
 @pytest.mark.parametrize("tran1", [False, True])
 @pytest.mark.parametrize("iso_a", [True, False])
 def test_colbits_mxm_vs_oracle(gb, name, mon, mul, masked, tran1, iso_a):
@@ -137,7 +161,8 @@ def test_colbits_mxm_vs_oracle(gb, name, mon, mul, masked, tran1, iso_a):
     Ao = _rand(rng, k, n, 0.05, iso=iso_a)
     Bo = _rand(rng, m if tran1 else n, n if tran1 else m, 0.02, iso=True)
     Mo = _rand(rng, k, m, 0.3, iso=masked == "value_iso")
-    Co = _rand(rng, k, m, 0.1, iso=True) if masked == "keep" else O.Csr.empty(k, m, "BOOL")
+    Co = _rand(rng, k, m, 0.1, iso=True) if masked in ("keep", "nullcomp", "nullcomp_replace") \
+        else O.Csr.empty(k, m, "BOOL")
     sr = getattr(gb.semiring, name)["BOOL"]
     Ag, Bg, Mg, Cg = _gbm(gb, Ao, iso_a), _gbm(gb, Bo, True), _gbm(gb, Mo, masked == "value_iso"), _gbm(gb, Co, True)
     Bx = Bg.T if tran1 else Bg
@@ -157,6 +182,14 @@ def test_colbits_mxm_vs_oracle(gb, name, mon, mul, masked, tran1, iso_a):
         elif masked == "value_replace":  # non-iso value mask: the general path
             Cg(Mg.V, replace=True) << Ag.mxm(Bx, sr)
             kw = dict(mask=Mo, replace=True)
+        elif masked in ("nullcomp", "nullcomp_replace"):
+            # ~NULL mask (C API: selects nothing), only reachable through the C ABI
+            rep = masked == "nullcomp_replace"
+            lib = gb.lib
+            desc = {(False, False): lib.GrB_DESC_C, (False, True): lib.GrB_DESC_CT1,
+                    (True, False): lib.GrB_DESC_RC, (True, True): lib.GrB_DESC_RCT1}[(rep, tran1)]
+            assert lib.GrB_mxm(Cg._h, None, None, sr._carg, Ag._h, Bg._h, desc) == 0
+            kw = dict(mask=None, mask_comp=True, replace=rep)
         else:  # mask without replace into a non-empty C: the general path
             Cg(Mg.S) << Ag.mxm(Bx, sr)
             kw = dict(mask=Mo, mask_struct=True)

@@ -557,7 +557,10 @@ def test_rmat_device_matches_oracle(gb, scale):
 @pytest.mark.parametrize("scale", [10, 14, 16])
 @pytest.mark.parametrize("direction", [0, 1, 2])  # auto (device-chosen), pull only, push only
 @pytest.mark.parametrize("heavy", [0, 8])  # push: default hub threshold, or hubs = rows > 8 edges
-def test_bfs_rmat_vs_oracle(gb, scale, direction, heavy):
+# lor_land: the notebook's semiring; any_pair: BASELINE.json configs[2]'s (semiring.py:174-203 binds
+# any_pair[BOOL] to GxB_ANY_PAIR_BOOL)
+@pytest.mark.parametrize("semiring", ["lor_land", "any_pair"])
+def test_bfs_rmat_vs_oracle(gb, scale, direction, heavy, semiring):
     if heavy and direction == 1:
         pytest.skip("pull does not use the hub split")
     G = O.rmat(scale, 16, 42)
@@ -566,13 +569,16 @@ def test_bfs_rmat_vs_oracle(gb, scale, direction, heavy):
     gb.set_knob("spmv_direction", direction)
     gb.set_knob("push_heavy", heavy)
     try:
-        _bfs_check(gb, G, A)
+        _bfs_check(gb, G, A, semiring)
     finally:
         gb.set_knob("spmv_direction", 0)
         gb.set_knob("push_heavy", 0)
 
 
-def _bfs_check(gb, G, A):
+def _bfs_check(gb, G, A, semiring="lor_land"):
+    sr = getattr(gb.semiring, semiring)
+    if semiring == "any_pair":
+        assert sr[bool].gb_name == "GxB_ANY_PAIR_BOOL"
     for src in [int(np.argmax(np.diff(G.indptr))), 0, G.nrows // 3]:
         lev_ref, _, _ = O.bfs_levels(G, src)
         vv = gb.Vector(gb.INT32, G.nrows)
@@ -582,7 +588,7 @@ def _bfs_check(gb, G, A):
         while True:
             d += 1
             vv(mask=q.V)[:] = d
-            q(~vv.S, replace=True) << q.vxm(A, gb.semiring.lor_land)
+            q(~vv.S, replace=True) << q.vxm(A, sr)
             if q.nvals == 0:
                 break
         got = np.zeros(G.nrows, np.int32)

@@ -46,6 +46,7 @@ BINOPS = [
     "BOR", "BAND", "BXOR", "BXNOR",
     "FIRSTI", "FIRSTI1", "FIRSTJ", "FIRSTJ1",
     "SECONDI", "SECONDI1", "SECONDJ", "SECONDJ1",
+    "ATAN2", "HYPOT", "FMOD", "REMAINDER", "LDEXP", "COPYSIGN",
 ]
 OPCODE = {n: i for i, n in enumerate(BINOPS)}
 BOOL_OUT = {"EQ", "NE", "GT", "LT", "GE", "LE"}
@@ -140,6 +141,11 @@ def binop_table():
     for op in sorted(POSITIONAL):
         for t in ["INT32", "INT64"]:
             add(f"GxB_{op}_{t}", op, None, t)
+    # floating-point only (reference binary.py:348; python-graphblas's BinaryOp._initialize
+    # coerces integer inputs onto them, binary.py:818-822, and deletes ldexp[FP32/FP64], :867)
+    for op in ["ATAN2", "HYPOT", "FMOD", "REMAINDER", "LDEXP", "COPYSIGN"]:
+        for t in ["FP32", "FP64"]:
+            add(f"GxB_{op}_{t}", op, t, t)
     return out
 
 
