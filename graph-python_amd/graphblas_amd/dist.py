@@ -128,6 +128,24 @@ class RowPanelAllGather:
         return out_rp, out_ci, out_vx, all_iso
 
 
+def concat_row_panels(torch, panels):
+    """The same assembly RowPanelAllGather.run performs, for panels already on this device
+    (several row shards driven from one process, e.g. the single-GPU tests of the sharded
+    product): panels = [(rowptr, colidx, values, iso)] in row order -> (rowptr, colidx,
+    values, iso) of the whole matrix; iso only when every panel is iso with equal bits."""
+    iso_bits = {RowPanelAllGather._value_bits(p[2]) for p in panels if p[3] and p[2].numel()}
+    all_iso = all(p[3] for p in panels) and len(iso_bits) <= 1
+    rps, cis, vxs, off = [torch.zeros(1, dtype=torch.int64, device=panels[0][0].device)], [], [], 0
+    for rp, ci, vx, iso in panels:
+        rps.append(rp[1:] + off)
+        cis.append(ci)
+        if not all_iso:
+            vxs.append(vx[:1].expand(ci.numel()) if iso else vx)
+        off += ci.numel()
+    vals = panels[0][2][:1].clone() if all_iso else torch.cat(vxs)
+    return torch.cat(rps), torch.cat(cis), vals, all_iso
+
+
 _TYPESTR = {0: "|b1", 1: "|i1", 2: "|u1", 3: "<i2", 4: "<u2", 5: "<i4", 6: "<u4", 7: "<i8", 8: "<u8",
             9: "<f4", 10: "<f8"}  # gbamd_type_code -> __cuda_array_interface__ typestr
 

@@ -1,0 +1,272 @@
+"""The 1-D row-sharded product paths of DESIGN.md §6, run through the HIP
+library on one GPU from one process: every shard of a world of W = 2 (and 3) is driven
+here in turn, and the exchange step is the same device-memory operation the RCCL
+collective performs -- the shards' slices are written into the full frontier / B panel
+through the zero-copy views (GxB_Vector_device_view / GxB_Matrix_colwords_view /
+GxB_Vector_bitmap_export+import / GxB_Matrix_import_device) on the library stream, then
+GxB_Vector_device_touch / GxB_Matrix_colwords_touch recount.  The collective itself is
+covered on CPU by tests/test_dist.py and tests/test_dist_spgemm.py (gloo, world size 2).
+
+Parity (bit-exact for the BFS levels, structure-exact and rtol 1e-9 for fp64 plus_times)
+against the oracle: O.bfs_levels, O.mxm.  Reference call shapes: core/matrix.py:2163-2251
+(mxv / mxm builders), notebooks/Example B.1 cell 8 (level BFS)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import oracle as O  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def env():
+    import torch
+
+    import graphblas_amd as gb
+
+    stream = torch.cuda.Stream()
+    gb.set_stream(stream)
+    yield gb, torch, stream
+    torch.cuda.synchronize()
+    gb.set_stream(None)
+
+
+def ok(rc, what):
+    assert rc == 0, f"{what}: GrB_Info {rc}"
+
+
+def _extract_int32(lib, v):
+    nv = ctypes.c_uint64()
+    ok(lib.GrB_Vector_nvals(ctypes.byref(nv), v), "nvals")
+    idx = np.empty(nv.value, np.uint64)
+    x = np.empty(nv.value, np.int32)
+    ok(lib.GrB_Vector_extractTuples_INT32(ctypes.c_void_p(idx.ctypes.data), ctypes.c_void_p(x.ctypes.data),
+                                          ctypes.byref(nv), v), "extract")
+    return idx.astype(np.int64), x
+
+
+@pytest.mark.parametrize("scale", [10, 12, 14])
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("exchange", ["view", "bitmap"])
+@pytest.mark.parametrize("semiring", ["GrB_LOR_LAND_SEMIRING_BOOL", "GxB_ANY_PAIR_BOOL"])
+def test_sharded_bfs_mxv_vs_oracle(env, scale, world, exchange, semiring):
+    """bench.py's N > 1 loop: rank r holds rows [lo, hi) of A^T and runs
+    v_r<qloc_r> = d;  qloc_r<!v_r.S, replace> = A^T_r lor.land q  (GrB_mxv, GrB_DESC_RSC)
+    then the frontier slices are gathered into q's bitmap (in place through the device view, or
+    GxB_Vector_bitmap_export/_import), as the RCCL all-gather does."""
+    gb, torch, stream = env
+    from graphblas_amd import device as gdev
+    from graphblas_amd import dist as gdist
+
+    lib = gb.lib
+    n = 1 << scale
+    G = O.rmat(scale, 16, 42)
+    deg = np.diff(G.indptr)
+    parts = [gdist.partition(n, world, r) for r in range(world)]
+    words, slot = parts[0]["words"], parts[0]["slot"]
+    AT, v, ql = [], [], []
+    for p in parts:
+        nloc = p["hi"] - p["lo"]
+        h = ctypes.c_void_p()
+        ok(lib.GxB_Matrix_rmat(ctypes.byref(h), scale, 16, 42, 0x100, 0, p["lo"], p["hi"]), "rmat shard")
+        AT.append(h)
+        for lst, t in ((v, lib.GrB_INT32), (ql, lib.GrB_BOOL)):
+            x = ctypes.c_void_p()
+            ok(lib.GrB_Vector_new(ctypes.byref(x), t, nloc), "new")
+            lst.append(x)
+    q = ctypes.c_void_p()
+    ok(lib.GrB_Vector_new(ctypes.byref(q), lib.GrB_BOOL, n), "q")
+    gathered = torch.zeros(slot * world, dtype=torch.int64, device="cuda")
+    sr = getattr(lib, semiring)
+    nv = ctypes.c_uint64()
+
+    def exchange_frontier(first=False):
+        # the first exchange of a BFS goes through GxB_Vector_bitmap_import, which makes q iso
+        # true (bench.py does the same); later ones rewrite q's words in place
+        if exchange == "view" and not first:
+            with torch.cuda.stream(stream):
+                qb = gdev.device_tensor(torch, gdev.vector_view(q).bitmap, words)
+                for r, p in enumerate(parts):
+                    cnt = p["hi_w"] - p["lo_w"]
+                    if cnt:
+                        qb[p["lo_w"]:p["hi_w"]].copy_(gdev.device_tensor(torch, gdev.vector_view(ql[r]).bitmap, cnt))
+            ok(lib.GxB_Vector_device_touch(q), "touch")
+        else:
+            for r, p in enumerate(parts):
+                cnt = p["hi_w"] - p["lo_w"]
+                if cnt:
+                    ok(lib.GxB_Vector_bitmap_export(ql[r], ctypes.c_void_p(gathered.data_ptr() + 8 * r * slot), cnt),
+                       "export")
+            ok(lib.GxB_Vector_bitmap_import(q, ctypes.c_void_p(gathered.data_ptr()), words), "import")
+
+    rng = np.random.default_rng(scale + world)
+    for src in [int(np.argmax(deg)), int(rng.choice(np.flatnonzero(deg > 0)))]:
+        for x in v + ql:
+            ok(lib.GrB_Vector_clear(x), "clear")
+        for r, p in enumerate(parts):
+            if p["lo"] <= src < p["hi"]:
+                ok(lib.GrB_Vector_setElement_BOOL(ql[r], True, src - p["lo"]), "root")
+        exchange_frontier(first=True)
+        d = 0
+        while True:
+            d += 1
+            for r, p in enumerate(parts):
+                ok(lib.GrB_Vector_assign_INT32(v[r], ql[r], None, d, lib.GrB_ALL, p["hi"] - p["lo"], None), "assign")
+            for r in range(world):
+                ok(lib.GrB_mxv(ql[r], v[r], None, sr, AT[r], q, lib.GrB_DESC_RSC), "mxv")
+            exchange_frontier()
+            ok(lib.GrB_Vector_nvals(ctypes.byref(nv), q), "nvals")
+            if nv.value == 0:
+                break
+        got = np.zeros(n, np.int32)
+        for r, p in enumerate(parts):
+            idx, lv = _extract_int32(lib, v[r])
+            got[idx + p["lo"]] = lv
+        lev, _, _ = O.bfs_levels(G, src)
+        assert np.array_equal(got, lev), f"source {src}"
+    for h in AT:
+        ok(lib.GrB_Matrix_free(ctypes.byref(h)), "free")
+    for h in v + ql + [q]:
+        ok(lib.GrB_Vector_free(ctypes.byref(h)), "free")
+
+
+@pytest.mark.parametrize("scale", [10, 13])
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("k", [7, 64])
+@pytest.mark.parametrize("semiring", ["GrB_LOR_LAND_SEMIRING_BOOL", "GxB_ANY_PAIR_BOOL"])
+def test_sharded_msbfs_mxm_vs_oracle(env, scale, world, k, semiring):
+    """bench.py config3_msbfs_sharded: per level
+    Vloc_r<Qloc_r.V> = d;  Qloc_r<!Vloc_r.S, replace> = Q lor.land (A^T_r)^T   (GrB_DESC_RSCT1)
+    then each shard's column words (k bits per vertex) are written into Q's words through
+    GxB_Matrix_colwords_view, and GxB_Matrix_colwords_touch recounts Q."""
+    gb, torch, stream = env
+    from graphblas_amd import device as gdev
+    from graphblas_amd import dist as gdist
+
+    lib = gb.lib
+    n = 1 << scale
+    G = O.rmat(scale, 16, 42)
+    deg = np.diff(G.indptr)
+    rng = np.random.default_rng(scale * 10 + k)
+    roots = rng.choice(np.flatnonzero(deg > 0), k, replace=False).astype(np.uint64)
+    roots[0] = int(np.argmax(deg))
+    parts = [gdist.partition(n, world, r) for r in range(world)]
+    AT, Ql, Vl = [], [], []
+    for p in parts:
+        nloc = p["hi"] - p["lo"]
+        h = ctypes.c_void_p()
+        ok(lib.GxB_Matrix_rmat(ctypes.byref(h), scale, 16, 42, 0x100, 0, p["lo"], p["hi"]), "rmat shard")
+        AT.append(h)
+        for lst, t in ((Ql, lib.GrB_BOOL), (Vl, lib.GrB_INT32)):
+            x = ctypes.c_void_p()
+            ok(lib.GrB_Matrix_new(ctypes.byref(x), t, k, nloc), "new")
+            lst.append(x)
+    Q = ctypes.c_void_p()
+    ok(lib.GrB_Matrix_new(ctypes.byref(Q), lib.GrB_BOOL, k, n), "Q")
+    qi = np.arange(k, dtype=np.uint64)
+    ok(lib.GxB_Matrix_build_Scalar_BOOL(Q, ctypes.c_void_p(qi.ctypes.data), ctypes.c_void_p(roots.ctypes.data), True,
+                                        k), "build Q")
+    keep = []
+    for r, p in enumerate(parts):
+        mine = (roots >= p["lo"]) & (roots < p["hi"])
+        li = np.flatnonzero(mine).astype(np.uint64)
+        lj = (roots[mine] - p["lo"]).astype(np.uint64)
+        keep += [li, lj]
+        if li.size:
+            ok(lib.GxB_Matrix_build_Scalar_BOOL(Ql[r], ctypes.c_void_p(li.ctypes.data), ctypes.c_void_p(lj.ctypes.data),
+                                                True, li.size), "build Qloc")
+    sr = getattr(lib, semiring)
+    nv = ctypes.c_uint64()
+    d = 0
+    while True:
+        d += 1
+        for r, p in enumerate(parts):
+            nloc = p["hi"] - p["lo"]
+            ok(lib.GrB_Matrix_assign_INT32(Vl[r], Ql[r], None, d, lib.GrB_ALL, k, lib.GrB_ALL, nloc, None), "stamp")
+        for r in range(world):
+            ok(lib.GrB_mxm(Ql[r], Vl[r], None, sr, Q, AT[r], lib.GrB_DESC_RSCT1), "mxm")
+        with torch.cuda.stream(stream):
+            qptr, qn = gdev.colwords_view(Q)
+            qw = gdev.device_tensor(torch, qptr, qn)
+            for r, p in enumerate(parts):
+                ptr, cnt = gdev.colwords_view(Ql[r])
+                qw[p["lo"]:p["lo"] + cnt].copy_(gdev.device_tensor(torch, ptr, cnt))
+        ok(lib.GxB_Matrix_colwords_touch(Q), "touch")
+        ok(lib.GrB_Matrix_nvals(ctypes.byref(nv), Q), "nvals")
+        if nv.value == 0:
+            break
+    got = np.zeros((k, n), np.int32)
+    for r, p in enumerate(parts):
+        ok(lib.GrB_Matrix_nvals(ctypes.byref(nv), Vl[r]), "nvals V")
+        m = nv.value
+        vi, vj, vx = np.empty(m, np.uint64), np.empty(m, np.uint64), np.empty(m, np.int32)
+        cnt = ctypes.c_uint64(m)
+        ok(lib.GrB_Matrix_extractTuples_INT32(ctypes.c_void_p(vi.ctypes.data), ctypes.c_void_p(vj.ctypes.data),
+                                              ctypes.c_void_p(vx.ctypes.data), ctypes.byref(cnt), Vl[r]), "extract")
+        got[vi.astype(np.int64), vj.astype(np.int64) + p["lo"]] = vx
+    for i, s in enumerate(roots):
+        lev, _, _ = O.bfs_levels(G, int(s))
+        assert np.array_equal(got[i], lev), f"root {s} (row {i})"
+    for h in AT + Ql + Vl + [Q]:
+        ok(lib.GrB_Matrix_free(ctypes.byref(h)), "free")
+
+
+@pytest.mark.parametrize("scale", [9, 11])
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("method", [0, 1])  # spgemm_method: 0 hash Gustavson (default), 1 ESC
+def test_sharded_spgemm_plus_times_vs_oracle(env, scale, world, method):
+    """bench.py config5_spgemm at N > 1: rank r holds rows [lo, hi) of A (FP64 U[0,1)), which is
+    also its panel of B; B is assembled from the row panels (dist.concat_row_panels, the assembly
+    RowPanelAllGather.run performs after its broadcasts) and imported with
+    GxB_Matrix_import_device; each rank then runs C_r = A_r plus.times B (GrB_mxm)."""
+    gb, torch, stream = env
+    from graphblas_amd import device as gdev
+    from graphblas_amd import dist as gdist
+
+    lib = gb.lib
+    n = 1 << scale
+    G = O.rmat(scale, 16, 42, values="FP64", value_seed=2)
+    parts = [gdist.partition(n, world, r) for r in range(world)]
+    A, panels = [], []
+    for p in parts:
+        h = ctypes.c_void_p()
+        ok(lib.GxB_Matrix_rmat(ctypes.byref(h), scale, 16, 42, 2, 2, p["lo"], p["hi"]), "rmat fp64 panel")
+        A.append(h)
+        va = gdev.matrix_view(h)
+        panels.append((gdev.device_tensor(torch, va.rowptr, va.nrows + 1),
+                       gdev.device_tensor(torch, va.colidx, va.nvals, "<i4"),
+                       gdev.device_tensor(torch, va.values, 1 if va.iso else va.nvals, "<f8"), bool(va.iso)))
+    with torch.cuda.stream(stream):
+        brp, bci, bvx, biso = gdist.concat_row_panels(torch, panels)
+    B = ctypes.c_void_p()
+    ok(lib.GxB_Matrix_import_device(ctypes.byref(B), lib.GrB_FP64, n, n, ctypes.c_void_p(brp.data_ptr()),
+                                    ctypes.c_void_p(bci.data_ptr()), ctypes.c_void_p(bvx.data_ptr()), bci.numel(),
+                                    bool(biso)), "import B")
+    gb.set_knob("spgemm_method", method)
+    try:
+        for r, p in enumerate(parts):
+            nloc = p["hi"] - p["lo"]
+            C = ctypes.c_void_p()
+            ok(lib.GrB_Matrix_new(ctypes.byref(C), lib.GrB_FP64, nloc, n), "C")
+            ok(lib.GrB_mxm(C, None, None, lib.GrB_PLUS_TIMES_SEMIRING_FP64, A[r], B, None), "mxm")
+            vc = gdev.matrix_view(C)
+            stream.synchronize()  # the views are read on torch's stream: wait for the library's
+            crp = gdev.device_tensor(torch, vc.rowptr, nloc + 1).cpu().numpy()
+            cci = gdev.device_tensor(torch, vc.colidx, vc.nvals, "<i4").cpu().numpy().astype(np.int64)
+            cvx = gdev.device_tensor(torch, vc.values, vc.nvals, "<f8").cpu().numpy()
+            lo, hi = p["lo"], p["hi"]
+            sub = O.Csr(nloc, n, "FP64", G.indptr[lo:hi + 1] - G.indptr[lo], G.indices[G.indptr[lo]:G.indptr[hi]],
+                        G.values[G.indptr[lo]:G.indptr[hi]])
+            ref = O.mxm(O.Csr.empty(nloc, n, "FP64"), sub, G, ("PLUS", "TIMES", "FP64"))
+            assert np.array_equal(crp, ref.indptr) and np.array_equal(cci, ref.indices), f"shard {r} structure"
+            if method == 1:  # ESC folds in ascending k like the oracle: bit-identical
+                assert np.array_equal(cvx, ref.values), f"shard {r} values"
+            else:
+                assert np.allclose(cvx, ref.values, rtol=1e-9, atol=0), f"shard {r} values"
+            ok(lib.GrB_Matrix_free(ctypes.byref(C)), "free C")
+    finally:
+        gb.set_knob("spgemm_method", 0)
+    for h in A + [B]:
+        ok(lib.GrB_Matrix_free(ctypes.byref(h)), "free")
