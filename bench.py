@@ -4,8 +4,10 @@ configs[2]; the metric "GTEPS + achieved HBM GB/s, masked mxm/mxv on R-MAT s22")
 
 One step = one full level-synchronous BFS from one of 16 seeded roots, exactly
 the reference notebook loop (notebooks/Example B.1 -- Level BFS.ipynb cell 8):
-    v<q.V>[:] = d ;  q<!v.S, replace> = q lor.land A ;  stop when q is empty
-issued through the C ABI of libgraphblas_amd.so (GrB_Vector_assign_INT32,
+    v<q.V>[:] = d ;  q<!v.S, replace> = q any.pair A ;  stop when q is empty
+with BASELINE.json configs[2]'s semiring any_pair[BOOL] = GxB_ANY_PAIR_BOOL (the notebook
+writes lor_land; `--semiring lor_land` swaps them, and the other one is reported as a
+secondary line), issued through the C ABI of libgraphblas_amd.so (GrB_Vector_assign_INT32,
 GrB_vxm with GrB_DESC_RSC, GrB_Vector_nvals).  The graph is generated on the
 device (GxB_Matrix_rmat) and its CSC cache is built before timing (ingest).
 
@@ -62,6 +64,10 @@ def parse():
     p.add_argument("--dist-backend", default="nccl")
     p.add_argument("--device", type=int, default=None, help="override LOCAL_RANK's device")
     p.add_argument("--knob", action="append", default=[], help="library knob key=value (ablations)")
+    p.add_argument("--semiring", default="any_pair", choices=["any_pair", "lor_land"],
+                   help="BFS semiring: any_pair (BASELINE.json configs[2]) or lor_land (the notebook's)")
+    p.add_argument("--cpu-secondary-seconds", type=float, default=8.0,
+                   help="bound of each secondary line's CPU-baseline sample")
     p.add_argument("--spgemm-scale", type=int, default=19, help="config 5 (unmasked fp64 SpGEMM) R-MAT scale")
     p.add_argument("--spgemm-steps", type=int, default=2)
     p.add_argument("--spgemm-warmup", type=int, default=1)
@@ -113,6 +119,45 @@ def _time_calls(torch, stream, fn, reps):
     return e0.elapsed_time(e1) / 1e3 / reps
 
 
+def _bfs_semiring(lib, args):
+    """any_pair[BOOL] -> GxB_ANY_PAIR_BOOL (BASELINE.json configs[2]; reference semiring.py:174-203),
+    lor_land[BOOL] -> GrB_LOR_LAND_SEMIRING_BOOL (the notebook's, Example B.1 cell 8)"""
+    return lib.GxB_ANY_PAIR_BOOL if args.semiring == "any_pair" else lib.GrB_LOR_LAND_SEMIRING_BOOL
+
+
+def _threads():
+    """all of this box's host cores given to the job (OMP_NUM_THREADS; the machine's count otherwise)"""
+    return int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+
+
+def _profile_traffic(name):
+    """HBM bytes per call of a committed per-workload profile (tools/pmc_passes.sh +
+    tools/pmc_table.py: 2 x FETCH_SIZE + WRITE_SIZE summed over the call's kernels)."""
+    path = os.path.join(ROOT, "profiles", name)
+    try:
+        return json.load(open(path))["hbm_bytes_per_call"], f"profiles/{name}"
+    except Exception:
+        return None, None
+
+
+def _roofline(alg_bytes, seconds, traffic=None, source=None, kernel=None):
+    ach = alg_bytes / seconds / 1e9
+    r = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
+         "traffic": traffic, "alg_bytes": alg_bytes}
+    if source:
+        r["traffic_source"] = source
+    if kernel:
+        r["kernel"] = kernel
+    return r
+
+
+def _sym_transpose(O, n, indptr, indices, values, dtype):
+    S = sp.csr_matrix((values, indices, indptr), shape=(n, n))
+    T = S.T.tocsr()
+    T.sort_indices()
+    return O.Csr(n, n, dtype, T.indptr, T.indices, T.data)
+
+
 def secondary_workloads(lib, torch, stream, O, args):
     """SURVEY 8(d) configs 2 and 4 on one GPU, reported beside the headline BFS line:
     * config 2's kernel: y = x plus.times A, fp64, dense x (vxm) -- on R-MAT s22 (com-Orkut is
@@ -124,11 +169,13 @@ def secondary_workloads(lib, torch, stream, O, args):
     out = {}
     # ---- config 2 kernel: plus_times fp64 SpMV, R-MAT s22 at edge factor 16 (the BFS graph)
     # and at edge factor 60 (nnz 235M: com-Orkut's nnz, 234M, whose file is not available)
-    out["config2_spmv_plus_times_fp64"] = config2_spmv(lib, torch, stream, args, args.scale, args.edge_factor)
+    out["config2_spmv_plus_times_fp64"] = config2_spmv(lib, torch, stream, args, args.scale, args.edge_factor, O,
+                                                       cpu=True)
     out["config2_spmv_plus_times_fp64_orkut_nnz"] = config2_spmv(lib, torch, stream, args, args.scale, 60)
     # ---- config 4: masked min_plus SpGEMM, R-MAT s20 (configs[3]) and s22 (north_star's target)
     for s4 in (20, 22):
-        out[f"config4_masked_spgemm_min_plus_int64_s{s4}"] = config4_masked_spgemm(lib, torch, stream, O, args, s4)
+        out[f"config4_masked_spgemm_min_plus_int64_s{s4}"] = config4_masked_spgemm(lib, torch, stream, O, args, s4,
+                                                                                   cpu=s4 == 22)
     return out
 
 
@@ -148,7 +195,7 @@ def config3_msbfs(lib, torch, stream, O, args, A, n, ap, ai, deg, roots16):
     ok(lib.GrB_Matrix_new(ctypes.byref(V), lib.GrB_INT32, K, n), "V")
     qi = np.arange(K, dtype=np.uint64)
     nv = ctypes.c_uint64()
-    sr, desc, grb_all = lib.GrB_LOR_LAND_SEMIRING_BOOL, lib.GrB_DESC_RSC, lib.GrB_ALL
+    sr, desc, grb_all = _bfs_semiring(lib, args), lib.GrB_DESC_RSC, lib.GrB_ALL
 
     def batch():
         ok(lib.GrB_Matrix_clear(Q), "clear Q")
@@ -202,7 +249,8 @@ def config3_msbfs(lib, torch, stream, O, args, A, n, ap, ai, deg, roots16):
     el = (time.perf_counter() - t0) / reps
     ok(lib.GrB_Matrix_free(ctypes.byref(Q)), "free Q")
     ok(lib.GrB_Matrix_free(ctypes.byref(V)), "free V")
-    return {"workload": f"multi-source level BFS, {K} roots at once: V<Q.V> = d; Q<!V.S,replace> = Q lor.land A "
+    return {"workload": f"multi-source level BFS, {K} roots at once: V<Q.V> = d; Q<!V.S,replace> = Q "
+                        f"{args.semiring.replace('_', '.')} A "
                         f"(GrB_Matrix_assign + masked GrB_mxm, Q/V {K} x n), R-MAT s{args.scale}",
             "roots": K, "levels": levels, "ms_per_batch": el * 1e3, "gteps": edges / el / 1e9,
             "edges": edges, "parity_vs_oracle_2_roots": parity}
@@ -236,7 +284,7 @@ def config3_msbfs_sharded(lib, torch, stream, O, args, dist, world, rank, AT, pa
     ex = gdist.BitmapAllGather(dist, {"slot": vslot}, world, "cuda")
     zero_copy = vslot * world == n and args.dist_backend == "nccl"
     nv = ctypes.c_uint64()
-    sr, desc, ALL = lib.GrB_LOR_LAND_SEMIRING_BOOL, lib.GrB_DESC_RSCT1, lib.GrB_ALL
+    sr, desc, ALL = _bfs_semiring(lib, args), lib.GrB_DESC_RSCT1, lib.GrB_ALL
 
     def exchange():
         ptr, cnt = gdev.colwords_view(Ql)
@@ -311,12 +359,13 @@ def config3_msbfs_sharded(lib, torch, stream, O, args, dist, world, rank, AT, pa
     for h in (Q, Ql, Vl):
         ok(lib.GrB_Matrix_free(ctypes.byref(h)), "free")
     return {"workload": f"multi-source level BFS, {K} roots at once, 1-D row shards x{world}: Vloc<Qloc.V> = d; "
-                        f"Qloc<!Vloc.S,replace> = Q lor.land (A^T shard)^T, column words all-gathered per level",
+                        f"Qloc<!Vloc.S,replace> = Q {args.semiring.replace('_', '.')} (A^T shard)^T, column words "
+                        f"all-gathered per level",
             "roots": K, "levels": levels, "ms_per_batch": el * 1e3, "gteps": edges / el / 1e9, "edges": edges,
             "parity_vs_oracle_root0": parity, "zero_copy": zero_copy}
 
 
-def config2_spmv(lib, torch, stream, args, scale, ef):
+def config2_spmv(lib, torch, stream, args, scale, ef, O=None, cpu=False):
     """y = x plus.times A, dense fp64 x, on R-MAT (scale, ef)."""
     sc = scale
     n = 1 << sc
@@ -357,17 +406,38 @@ def config2_spmv(lib, torch, stream, args, scale, ef):
     parity2 = bool(np.array_equal(present, np.diff(S.tocsc().indptr) > 0) and
                    np.allclose(got, ref, rtol=1e-6, atol=1e-9))
     by = 12 * nnz + 8 * (n + 1) + 16 * n
+    traffic, src = _profile_traffic(f"r03_config2_s{sc}_pmc.json") if ef == 16 else (None, None)
     res = {
         "workload": f"y = x plus.times A (GrB_vxm, dense fp64 x) on R-MAT s{sc} ef {ef} fp64 U[0,1) "
                     f"(com-Orkut stand-in)",
         "nnz": nnz, "ms": t * 1e3, "gteps": nnz / t / 1e9, "alg_bytes": by, "hbm_GBs": by / t / 1e9,
-        "parity_vs_scipy": parity2}
+        "parity_vs_scipy": parity2,
+        "roofline": _roofline(by, t, traffic, src, "k_spmv_words + k_spmv_fold (one call)")}
+    if cpu and not args.no_cpu_baseline:
+        # the same SpMV on all host cores (oracle or_spmv_plus_times_fp64_par: pull over A^T), repeated
+        # for about --cpu-secondary-seconds
+        th = _threads()
+        AT = _sym_transpose(O, n, ap.astype(np.int64), ai.astype(np.int64), ax, "FP64")
+        yc, pc = O.spmv_plus_times_fp64_par(AT, xv, th)
+        cpu_ok = bool(np.array_equal(pc, present) and np.allclose(yc, ref, rtol=1e-9, atol=0))
+        reps, tc = 0, 0.0
+        while tc < args.cpu_secondary_seconds and reps < 1000:
+            t1 = time.perf_counter()
+            O.spmv_plus_times_fp64_par(AT, xv, th)
+            tc += time.perf_counter() - t1
+            reps += 1
+        res["cpu_baseline"] = {"value": nnz * reps / tc / 1e9, "unit": "GTEPS", "cores": th, "kind": "port",
+                               "ms": tc / reps * 1e3, "hbm_GBs": by * reps / tc / 1e9, "matches_scipy": cpu_ok,
+                               "sample": f"{reps} full SpMVs of the same matrix and x, {tc:.1f} s: pull over A^T "
+                                         f"on {th} host threads (oracle or_spmv_plus_times_fp64_par, OpenMP; "
+                                         f"not SuiteSparse)"}
+        del AT
     for h in (A, x, y):
         lib.GrB_Matrix_free(ctypes.byref(h))
     return res
 
 
-def config4_masked_spgemm(lib, torch, stream, O, args, s4):
+def config4_masked_spgemm(lib, torch, stream, O, args, s4, cpu=False):
     """C<A.S> = A min.plus A (GrB_mxm, GrB_DESC_S), INT64 weights in
     [1,255] on R-MAT scale s4; parity vs the oracle on 256 sampled rows (bit-exact)."""
     n4 = 1 << s4
@@ -422,13 +492,44 @@ def config4_masked_spgemm(lib, torch, stream, O, args, s4):
     by4 = 2 * (12 * nnz4 + 8 * (n4 + 1)) + 4 * nnz4 + 8 * (n4 + 1) + 12 * nnzc + 8 * (n4 + 1)
     for h in (B, C):
         lib.GrB_Matrix_free(ctypes.byref(h))
-    return {
+    traffic, src = _profile_traffic(f"r03_config4_s{s4}_pmc.json")
+    res = {
         "workload": f"C<A.S> = A min.plus A (GrB_mxm, GrB_DESC_S), R-MAT s{s4}, INT64 weights in [1,255]",
         "nnz_A": nnz4, "nnz_C": nnzc, "ms": t4 * 1e3, "gteps": work / t4 / 1e9,
         "gteps_def": "sum over mask entries (i,j) of deg_out(i) + deg_in(j), per second",
         "intersection_keys_per_s": inter / t4,
         "intersection_def": "sum over mask entries of min(deg_out(i), deg_in(j)): the keys the dot streams",
-        "alg_bytes": by4, "hbm_GBs": by4 / t4 / 1e9, "parity_vs_oracle_256_rows": parity4}
+        "alg_bytes": by4, "hbm_GBs": by4 / t4 / 1e9, "parity_vs_oracle_256_rows": parity4,
+        "roofline": _roofline(by4, t4, traffic, src, "masked dot kernels (k_dot_task, k_dot_small, ...; one call)")}
+    if cpu and not args.no_cpu_baseline:
+        # the masked dot on all host cores (oracle or_masked_dot_min_plus_int64_par: per mask entry a
+        # sorted merge / galloping of A(i,:) with A(:,j)) over the mask rows [0, r1) -- labels are
+        # scrambled, so a leading block of rows is a random sample -- doubling r1 until the sample takes
+        # --cpu-secondary-seconds; GTEPS by the same definition as the GPU line
+        th = _threads()
+        Ac = O.Csr(n4, n4, "INT64", bp, bi, bx)
+        AT = _sym_transpose(O, n4, bp, bi, bx, "INT64")
+        r1 = max(64, n4 >> 12)
+        while True:
+            t1 = time.perf_counter()
+            vals_c, pres_c, nc_c, work_c = O.masked_dot_min_plus_int64_par(Ac, AT, 0, r1, th)
+            tc = time.perf_counter() - t1
+            if tc >= args.cpu_secondary_seconds / 2 or r1 >= n4:
+                break
+            r1 = min(n4, r1 * 2)
+        # the CPU sample's entries equal the GPU's C on those rows (bit-exact)
+        e1 = int(bp[r1])
+        cpu_ok = bool(int(cp[r1]) == int(pres_c.sum()) and
+                      np.array_equal(ci[:int(cp[r1])].astype(np.int64), bi[:e1][pres_c]) and
+                      np.array_equal(cx[:int(cp[r1])], vals_c[pres_c]))
+        res["cpu_baseline"] = {"value": work_c / tc / 1e9, "unit": "GTEPS", "cores": th, "kind": "port",
+                               "matches_gpu": cpu_ok,
+                               "sample": f"mask rows [0, {r1}) of {n4} ({e1} mask entries, {work_c:.3e} list "
+                                         f"elements), {tc:.1f} s on {th} host threads: per mask entry a sorted "
+                                         f"merge / galloping dot (oracle or_masked_dot_min_plus_int64_par, OpenMP; "
+                                         f"not SuiteSparse)"}
+        del Ac, AT
+    return res
 
 
 def config5_spgemm(lib, torch, stream, dist, world, rank, args):
@@ -617,7 +718,7 @@ def main():
     rng = np.random.default_rng(args.seed)
     roots = rng.choice(np.flatnonzero(deg > 0), 16, replace=False)  # Graph500: roots with out-edges
 
-    sr = lib.GrB_LOR_LAND_SEMIRING_BOOL
+    sr_box = [_bfs_semiring(lib, args)]  # the BFS semiring (swapped for the other-semiring line)
     desc = lib.GrB_DESC_RSC
     grb_all = lib.GrB_ALL
     q = ctypes.c_void_p()
@@ -672,7 +773,7 @@ def main():
                     with torch.cuda.stream(stream):
                         torch.cuda._sleep(SLEEP_CYCLES)
                     e0.record(stream)
-                ok(lib.GrB_vxm(q, v, None, sr, q, A, desc), "vxm")
+                ok(lib.GrB_vxm(q, v, None, sr_box[0], q, A, desc), "vxm")
                 if timing:
                     e1.record(stream)
                     ev_pairs.append((e0, e1))
@@ -682,7 +783,7 @@ def main():
                     with torch.cuda.stream(stream):
                         torch.cuda._sleep(SLEEP_CYCLES)
                     e0.record(stream)
-                ok(lib.GrB_mxv(qloc, v, None, sr, A, q, desc), "mxv")
+                ok(lib.GrB_mxv(qloc, v, None, sr_box[0], A, q, desc), "mxv")
                 if timing:
                     e1.record(stream)
                     ev_pairs.append((e0, e1))
@@ -796,6 +897,37 @@ def main():
         del xs, ys
 
     secondary = {}
+    # the same timed loop with the other boolean semiring (BASELINE.json names any_pair, the notebook
+    # lor_land): both take the iso-result SpMV; parity of root 0's levels vs the oracle
+    other = "lor_land" if args.semiring == "any_pair" else "any_pair"
+    sr_box[0] = lib.GrB_LOR_LAND_SEMIRING_BOOL if other == "lor_land" else lib.GxB_ANY_PAIR_BOOL
+    bfs(roots[0], False)
+    e0_, idx0, lv0 = reached_edges()
+    par_other = None
+    if world == 1:
+        got = np.zeros(n, np.int32)
+        got[idx0] = lv0
+        par_other = bool(np.array_equal(got, lev_ref))
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for s in range(len(roots)):
+        bfs(roots[s], False)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el_o = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([el_o], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el_o = float(tt.item())
+    sr_box[0] = _bfs_semiring(lib, args)
+    secondary[f"config3_level_bfs_{other}"] = {
+        "workload": f"the headline loop with {other}[BOOL] "
+                    f"({'GrB_LOR_LAND_SEMIRING_BOOL' if other == 'lor_land' else 'GxB_ANY_PAIR_BOOL'}), "
+                    f"the {len(roots)} roots once each", "gteps": sum(edges) / el_o / 1e9,
+        "ms_per_bfs": el_o / len(roots) * 1e3, "parity_vs_oracle_root0": par_other}
     if world > 1 and args.msbfs_sharded:
         secondary["config3_msbfs_64_roots_sharded"] = config3_msbfs_sharded(
             lib, torch, stream, O, args, dist, world, rank, A, part, deg, roots)
@@ -859,7 +991,9 @@ def main():
             "vs_baseline": None,
             "dtype": "bool",
             "data": "synthetic (Graph500-style R-MAT .57/.19/.19/.05, generated on device, seed 42)",
-            "config": {"workload": f"level-BFS q<!v.S,replace> = q lor.land A (GrB_vxm; GrB_mxv on A^T "
+            "config": {"workload": f"level-BFS q<!v.S,replace> = q {args.semiring.replace('_', '.')} A "
+                                   f"({'GxB_ANY_PAIR_BOOL' if args.semiring == 'any_pair' else 'GrB_LOR_LAND_SEMIRING_BOOL'}"
+                                   f"; GrB_vxm, GrB_mxv on A^T "
                                    f"shards for N>1), R-MAT scale {scale}, edge factor {args.edge_factor}, "
                                    f"16 roots", "n": n, "nnz": nnz,
                        "parallelism": f"1-D row shards x{world}" if world > 1 else "single GPU"},

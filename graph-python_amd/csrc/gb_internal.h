@@ -95,6 +95,11 @@ struct GB_Matrix_opaque {
     int64_t hub_n[2], hub_H[2];
     // cached bitmaps of the non-empty rows of the CSR (0) / CSC (1)
     uint64_t *rows_ne[2];
+    // cached hub-first probes of the CSR (0) / CSC (1) orientation (gb_view_pullfirst,
+    // gb_mxv.hip): per row its neighbour with the most entries in the other orientation, and
+    // the row's own length in the other orientation (saturated to 32 bits)
+    int32_t *pfirst[2];
+    uint32_t *pdeg[2];
     // cached long-row chunk tables (general SpMV, gb_mxv.hip)
     int32_t *long_tab[2];
     int64_t long_n[2];
@@ -276,6 +281,8 @@ struct gb_csr_view {
     const int32_t *hubs = nullptr;
     int64_t nhubs = 0, hub_H = 0;
     const uint64_t *nonempty = nullptr;  // bitmap of rows with entries (when attached)
+    const int32_t *pfirst = nullptr;     // hub-first probe per row (when attached; -1: empty row)
+    const uint32_t *pdeg = nullptr;      // row length in the other orientation (when attached)
     const int32_t *lchunks = nullptr;    // long-row chunks (row, piece) of the general SpMV (when attached)
     int64_t nlchunks = -1;
     // column-sliced copy (when attached): 8 slice CSRs, int32 row pointers [8][nrows+1]
@@ -293,6 +300,9 @@ void gb_get_csr(gb_csr_view &v, GB_Obj *A);
 void gb_view_hubs(gb_csr_view &v, GB_Obj *A, int orient, int64_t H);
 // attach the cached non-empty-rows bitmap of matrix A's orientation to v
 void gb_view_nonempty(gb_csr_view &v, GB_Obj *A, int orient);
+// attach the cached hub-first probes of A's orientation (other_rowptr: the other orientation's
+// row pointers, other_n rows) -- the iso pull tests a row's best-connected neighbour first
+void gb_view_pullfirst(gb_csr_view &v, GB_Obj *A, int orient, const int64_t *other_rowptr, int64_t other_n);
 void gb_view_long_rows(gb_csr_view &v, GB_Obj *A, int orient);
 // attach (building on first use) the column-sliced copy of matrix A's orientation
 void gb_view_slices(gb_csr_view &v, GB_Obj *A, int orient);

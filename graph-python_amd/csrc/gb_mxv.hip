@@ -431,7 +431,9 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
                                                       const int64_t *__restrict__ hprow, long long &mfn,
                                                       int p1_steps, int cap0, const uint64_t *__restrict__ rne,
                                                       const uint64_t *__restrict__ qbits, const gb_asg_dev &g,
-                                                      long long &adelta, int dbg = 0) {
+                                                      long long &adelta, int dbg = 0,
+                                                      const int32_t *__restrict__ pf = nullptr,
+                                                      const uint32_t *__restrict__ pdeg = nullptr) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -458,22 +460,42 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
         }
         bool live[PULL_U], found[PULL_U];
         int64_t p[PULL_U], p1[PULL_U];
-        // row bounds are loaded for every row, independently of the mask word
-#pragma unroll
-        for (int u = 0; u < PULL_U; u++) {
-            const int64_t r = ((w0 + u) << 6) + lane;
-            p[u] = p1[u] = 0;
-            if (r < nrows) {
-                p[u] = rowptr[r];
-                p1[u] = rowptr[r + 1];
-            }
-        }
-        int32_t dg[PULL_U];
+        int64_t dg[PULL_U];
 #pragma unroll
         for (int u = 0; u < PULL_U; u++) {
             live[u] = (__shfl(mine, u, 64) >> lane) & 1ULL;
             found[u] = false;
-            dg[u] = (int32_t)(p1[u] - p[u]);
+        }
+        if (pf) {
+            // hub-first probe: each open row tests its best-connected neighbour (one coalesced
+            // 4-byte load per row); rows it settles never read their row bounds or edges
+            int32_t kf[PULL_U];
+#pragma unroll
+            for (int u = 0; u < PULL_U; u++) kf[u] = live[u] ? pf[((w0 + u) << 6) + lane] : -1;
+#pragma unroll
+            for (int u = 0; u < PULL_U; u++) found[u] = kf[u] >= 0 && gb_bit(ubits, kf[u]);
+#pragma unroll
+            for (int u = 0; u < PULL_U; u++) {
+                const int64_t r = ((w0 + u) << 6) + lane;
+                p[u] = p1[u] = 0;
+                if (live[u] && !found[u] && r < nrows) {
+                    p[u] = rowptr[r];
+                    p1[u] = rowptr[r + 1];
+                }
+                dg[u] = (hprow && found[u]) ? (int64_t)pdeg[r] : p1[u] - p[u];
+            }
+        } else {
+            // row bounds are loaded for every row, independently of the mask word
+#pragma unroll
+            for (int u = 0; u < PULL_U; u++) {
+                const int64_t r = ((w0 + u) << 6) + lane;
+                p[u] = p1[u] = 0;
+                if (r < nrows) {
+                    p[u] = rowptr[r];
+                    p1[u] = rowptr[r + 1];
+                }
+                dg[u] = p1[u] - p[u];
+            }
         }
         for (int it = 0; it < p1_steps; it++) {
             bool go[PULL_U], any = false;
@@ -655,6 +677,8 @@ struct gb_iso_args {
                                     // 16 pull without its segment list, 32 pull steps without probes (wrong results)
     bool packed;                    // one-round finish (iso_finish_packed): n < 2^27
     const uint64_t *rows_nonempty;  // pull rows with entries (nullptr: all)
+    const int32_t *pfirst;          // hub-first probe per pull row (nullptr: none)
+    const uint32_t *pdeg;           // push-orientation length per pull row (the hint of found rows)
     // fused deferred assign (gb_asg): w<q>(:) = x with q = u (asg.bits nullptr: none)
     gb_asg_dev asg;
     const void *asg_qiso;
@@ -1147,7 +1171,8 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
                             (unsigned long long *)tbits, L, a.hprow, mfn, qbits, a.asg, adelta);
     else
         cnt = gb_pull_iso_phase(nrows, rowptr, colidx, ubits, mbits, mcomp, tbits, L, a.hprow, mfn, a.p1_steps,
-                                a.cap0, a.rows_nonempty, qbits, a.asg, adelta, a.dbg);
+                                a.cap0, a.rows_nonempty, qbits, a.asg, adelta, a.dbg,
+                                (a.pfirst && (!a.hprow || a.pdeg)) ? a.pfirst : nullptr, a.pdeg);
     if (a.packed) {
         iso_finish_packed(cnt, mfn, adelta, tcount, gst, a);
         return;
@@ -1252,6 +1277,60 @@ void gb_view_nonempty(gb_csr_view &v, GB_Obj *A, int orient) {
     v.nonempty = A->rows_ne[orient];
 }
 
+// hub-first probes: a wave per row picks the neighbour with the longest row in the other
+// orientation (ties: the smaller index) -- in a level BFS that neighbour is the one most
+// likely to be in the frontier, so most rows the pull settles are settled by it -- and
+// stores the row's own length in the other orientation (the next-frontier hint of a row
+// settled without reading its bounds)
+__global__ __launch_bounds__(256) void k_pull_first(int64_t n, const int64_t *__restrict__ rp,
+                                                    const int32_t *__restrict__ ci,
+                                                    const int64_t *__restrict__ orp, int64_t on,
+                                                    int32_t *__restrict__ pf, uint32_t *__restrict__ pdeg) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t j = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; j < n; j += nwaves) {
+        int64_t bd = -1;
+        int32_t bi = -1;
+        for (int64_t e = rp[j] + lane; e < rp[j + 1]; e += 64) {
+            const int32_t i = ci[e];
+            const int64_t d = orp[i + 1] - orp[i];
+            if (d > bd || (d == bd && i < bi)) {
+                bd = d;
+                bi = i;
+            }
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            const int64_t od = __shfl_xor(bd, off, 64);
+            const int32_t oi = __shfl_xor(bi, off, 64);
+            if (od > bd || (od == bd && oi >= 0 && (bi < 0 || oi < bi))) {
+                bd = od;
+                bi = oi;
+            }
+        }
+        if (lane == 0) {
+            pf[j] = bi;
+            if (pdeg) {
+                const int64_t d = j < on ? orp[j + 1] - orp[j] : 0;
+                pdeg[j] = (uint32_t)(d < 0xFFFFFFFFLL ? d : 0xFFFFFFFFLL);
+            }
+        }
+    }
+}
+
+void gb_view_pullfirst(gb_csr_view &v, GB_Obj *A, int orient, const int64_t *other_rowptr, int64_t other_n) {
+    if (A->kind != GB_KIND_MATRIX || v.nrows == 0) return;
+    if (!A->pfirst[orient]) {
+        A->pfirst[orient] = gb_malloc_n<int32_t>(v.nrows);
+        A->pdeg[orient] = gb_malloc_n<uint32_t>(v.nrows);
+        const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((v.nrows + 3) / 4, 65535));
+        hipLaunchKernelGGL(k_pull_first, dim3(g), dim3(256), 0, gb_stream(), v.nrows, v.rowptr, v.colidx,
+                           other_rowptr, other_n, A->pfirst[orient], A->pdeg[orient]);
+        GB_LAUNCH_CHECK();
+    }
+    v.pfirst = A->pfirst[orient];
+    v.pdeg = A->pdeg[orient];
+}
+
 // constant value of an iso result: mult(a0, u0) (positional ops are never iso)
 template <class SR, class X, class Z, bool FLIP>
 __global__ void k_iso_value(SR sr, const X *avals, const X *uvals, Z *out) {
@@ -1353,6 +1432,8 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             args.cap0 = (int)gb_knob("pull_cap");
             if (args.cap0 <= 0) args.cap0 = 16;
             args.rows_nonempty = A.nonempty;
+            args.pfirst = A.pfirst;
+            args.pdeg = A.pdeg;
             // the result's iso value: evaluated by the finishing block when z is x's type or bool
             const bool eval_ok = info.zcode == info.xcode || info.zcode == GBAMD_T_BOOL;
             if (eval_ok) {

@@ -128,6 +128,10 @@ void gb_drop_transpose(GB_Obj *A) {
         A->hub_n[o] = A->hub_H[o] = 0;
         gb_free(A->rows_ne[o]);
         A->rows_ne[o] = nullptr;
+        gb_free(A->pfirst[o]);
+        gb_free(A->pdeg[o]);
+        A->pfirst[o] = nullptr;
+        A->pdeg[o] = nullptr;
         gb_free(A->long_tab[o]);
         A->long_tab[o] = nullptr;
         A->long_n[o] = 0;

@@ -88,6 +88,7 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
         int64_t H = gb_knob("push_heavy");
         gb_view_hubs(pv, A, use_csc ? 0 : 1, H > 0 ? H : 512);
         push = &pv;
+        if (gb_knob("pull_first") != 1) gb_view_pullfirst(av, A, use_csc ? 1 : 0, pv.rowptr, pv.nrows);
     }
     gb_vec_result T;
     if (w->kind != GB_KIND_MATRIX) {

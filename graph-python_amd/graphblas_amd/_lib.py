@@ -14,6 +14,16 @@ import os
 
 from . import _builtins
 
+# One HIP runtime per process: torch ships its own libamdhip64 / libhsa-runtime64.  When this
+# library is loaded first, its DT_NEEDED pulls /opt/rocm's runtime in and torch's later CUDA
+# init finds "no ROCm-capable device"; importing torch first makes the dynamic loader resolve
+# our libamdhip64.so.7 to the runtime torch already loaded (bench.py, the device views and the
+# RCCL exchange all share torch's stream / device with the library).
+try:  # torch is optional (plumbing only)
+    import torch  # noqa: F401
+except Exception:
+    pass
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GRAPHBLAS_AMD_LIB", os.path.join(_HERE, "libgraphblas_amd.so"))
 

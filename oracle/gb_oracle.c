@@ -793,3 +793,90 @@ int or_bfs_graphblas(const or_csr *A, int64_t src, int32_t *levels, int64_t *edg
     if (edges) *edges = e;
     return d;
 }
+
+/* ================================================================== CPU baselines
+ * (bench.py cpu_baseline legs of SURVEY §8(d) configs 2 and 4; not a parity oracle:
+ * tests/test_cpu_baseline.py checks them against or_mxm and scipy) */
+
+/* y = x plus.times A (GrB_vxm with a dense FP64 x), pulled over AT = A^T (rows of AT are
+ * the output positions); each output folds its column in ascending row order, nthreads
+ * host threads.  present[j] = 1 iff column j of A holds an entry. */
+void or_spmv_plus_times_fp64_par(const or_csr *AT, const double *x, double *y, uint8_t *present, int nthreads) {
+    const int64_t n = AT->nrows;
+    const double *ax = (const double *)AT->x;
+    if (nthreads < 1) nthreads = 1;
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1024)
+    for (int64_t j = 0; j < n; j++) {
+        double s = 0.0;
+        const int64_t p0 = AT->p[j], p1 = AT->p[j + 1];
+        for (int64_t p = p0; p < p1; p++) s += ax[p] * x[AT->j[p]];
+        y[j] = s;
+        present[j] = p1 > p0;
+    }
+}
+
+/* first position in j[lo, hi) with j[pos] >= key (galloping from lo, then binary search) */
+static int64_t gallop(const int64_t *j, int64_t lo, int64_t hi, int64_t key) {
+    int64_t step = 1, a = lo, b = lo;
+    while (b < hi && j[b] < key) {
+        a = b + 1;
+        b = lo + step;
+        step <<= 1;
+    }
+    if (b > hi) b = hi;
+    while (a < b) {
+        const int64_t m = (a + b) >> 1;
+        if (j[m] < key) a = m + 1;
+        else b = m;
+    }
+    return a;
+}
+
+/* C<A.S> = A min.+ A (INT64) over the mask rows [row0, row1): for each mask entry (i, j) the
+ * intersection of A(i,:) with A(:,j) = AT(j,:) by a sorted merge, galloping through the longer
+ * list when the lengths differ by 8x or more -- the dot form a CPU GraphBLAS library runs for
+ * a masked mxm whose mask is sparse (SuiteSparse dot3).  Integer wrap as GB_ADD.  cvals /
+ * present are indexed by the mask entry's position minus A->p[row0].  Returns the number of
+ * entries of C in those rows; *work = sum over the mask entries of deg_out(i) + deg_in(j)
+ * (the GTEPS numerator of SURVEY §8(d) config 4). */
+int64_t or_masked_dot_min_plus_int64_par(const or_csr *A, const or_csr *AT, int64_t row0, int64_t row1,
+                                         int64_t *cvals, uint8_t *present, int64_t *work, int nthreads) {
+    const int64_t *ax = (const int64_t *)A->x, *tx = (const int64_t *)AT->x;
+    const int64_t base = A->p[row0];
+    int64_t nc = 0, wk = 0;
+    if (nthreads < 1) nthreads = 1;
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 64) reduction(+ : nc, wk)
+    for (int64_t i = row0; i < row1; i++) {
+        const int64_t a0 = A->p[i], a1 = A->p[i + 1];
+        for (int64_t e = a0; e < a1; e++) {
+            const int64_t jcol = A->j[e];
+            int64_t p = a0, q = AT->p[jcol];
+            const int64_t pe = a1, qe = AT->p[jcol + 1];
+            wk += (pe - p) + (qe - q);
+            int have = 0;
+            int64_t best = INT64_MAX;
+            const int64_t la = pe - p, lb = qe - q;
+            while (p < pe && q < qe) {
+                const int64_t ka = A->j[p], kb = AT->j[q];
+                if (ka == kb) {
+                    const int64_t z = (int64_t)((uint64_t)ax[p] + (uint64_t)tx[q]);
+                    if (!have || z < best) best = z;
+                    have = 1;
+                    p++;
+                    q++;
+                } else if (ka < kb) {
+                    p = la >= 8 * lb ? gallop(A->j, p + 1, pe, kb) : p + 1;
+                } else {
+                    q = lb >= 8 * la ? gallop(AT->j, q + 1, qe, ka) : q + 1;
+                }
+            }
+            present[e - base] = (uint8_t)have;
+            if (have) {
+                cvals[e - base] = best;
+                nc++;
+            }
+        }
+    }
+    if (work) *work = wk;
+    return nc;
+}

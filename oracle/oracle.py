@@ -288,6 +288,32 @@ def bfs_levels_par(A, AT, src, nthreads):
     return lev, nl, edges.value
 
 
+def spmv_plus_times_fp64_par(AT, x, nthreads):
+    """CPU baseline (config 2): y = x plus.times A over AT = A^T (FP64 Csr); -> (y, present)."""
+    y = np.empty(AT.nrows, np.float64)
+    present = np.empty(AT.nrows, np.uint8)
+    x = np.ascontiguousarray(x, np.float64)
+    lib().or_spmv_plus_times_fp64_par(ctypes.byref(AT._c()), x.ctypes.data_as(ctypes.c_void_p),
+                                      y.ctypes.data_as(ctypes.c_void_p), present.ctypes.data_as(ctypes.c_void_p),
+                                      ctypes.c_int(nthreads))
+    return y, present.astype(bool)
+
+
+def masked_dot_min_plus_int64_par(A, AT, row0, row1, nthreads):
+    """CPU baseline (config 4): C<A.S> = A min.+ A over mask rows [row0, row1) (INT64 Csr A and
+    AT = A^T); -> (values per mask entry, present per mask entry, nnz(C) rows, work)."""
+    m = int(A.indptr[row1] - A.indptr[row0])
+    vals = np.zeros(max(m, 1), np.int64)
+    present = np.zeros(max(m, 1), np.uint8)
+    work = ctypes.c_int64(0)
+    f = lib().or_masked_dot_min_plus_int64_par
+    f.restype = ctypes.c_int64
+    nc = f(ctypes.byref(A._c()), ctypes.byref(AT._c()), ctypes.c_int64(row0), ctypes.c_int64(row1),
+           vals.ctypes.data_as(ctypes.c_void_p), present.ctypes.data_as(ctypes.c_void_p), ctypes.byref(work),
+           ctypes.c_int(nthreads))
+    return vals[:m], present[:m].astype(bool), int(nc), work.value
+
+
 def bfs_graphblas(A, src):
     """The Level-BFS loop of the reference notebook (Example B.1 cell 8) through or_mxm:
        v[:](mask=q.V) << d ; q(~v.S, replace) << q.vxm(A, lor_land) ; stop when q empty."""
