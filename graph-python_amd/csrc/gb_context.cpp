@@ -1,3 +1,5 @@
+#include <chrono>
+#include <cstdio>
 // gb_context.cpp -- library context: init/finalize, the HIP stream, the
 // stream-ordered device memory pool, error plumbing, descriptors, builtin
 // object lookup.  (Replaces SuiteSparse's GrB_init / GxB_Global / GrB_Descriptor
@@ -146,6 +148,34 @@ unsigned long long *gb_device_state() {
         GB_HIP(hipDeviceSynchronize());
     }
     return st;
+}
+
+// ---- host-time probes (gb_internal.h)
+bool g_hprof_on = getenv("GRAPHBLAS_AMD_HPROF") != nullptr;
+namespace {
+struct hprof_slot {
+    std::atomic<int64_t> ns{0}, calls{0};
+    const char *name = nullptr;
+};
+hprof_slot g_hprof[32];
+struct hprof_print {
+    ~hprof_print() {
+        if (!g_hprof_on) return;
+        for (auto &s : g_hprof)
+            if (s.name && s.calls.load())
+                fprintf(stderr, "[hprof] %-28s calls %9lld  mean %8.2f us\n", s.name, (long long)s.calls.load(),
+                        s.ns.load() / 1e3 / (double)s.calls.load());
+    }
+} g_hprof_print;
+}  // namespace
+int64_t gb_hprof_now() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+void gb_hprof_add(int slot, const char *name, int64_t ns) {
+    g_hprof[slot].name = name;
+    g_hprof[slot].ns += ns;
+    g_hprof[slot].calls += 1;
 }
 
 int64_t gb_knob(const char *key) {

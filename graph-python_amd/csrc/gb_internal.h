@@ -95,10 +95,11 @@ struct GB_Matrix_opaque {
     int64_t hub_n[2], hub_H[2];
     // cached bitmaps of the non-empty rows of the CSR (0) / CSC (1)
     uint64_t *rows_ne[2];
-    // cached hub-first probes of the CSR (0) / CSC (1) orientation (gb_view_pullfirst,
-    // gb_mxv.hip): per row its neighbour with the most entries in the other orientation, and
+    // cached pull heads of the CSR (0) / CSC (1) orientation (gb_view_pullfirst, gb_mxv.hip):
+    // per row 4 int32 -- its neighbours with the most entries in the other orientation
+    // first, the whole row when it has at most 4 (padding -1), else 3 of them and -2 -- and
     // the row's own length in the other orientation (saturated to 32 bits)
-    int32_t *pfirst[2];
+    int32_t *phead[2];
     uint32_t *pdeg[2];
     // cached long-row chunk tables (general SpMV, gb_mxv.hip)
     int32_t *long_tab[2];
@@ -193,6 +194,23 @@ GrB_Info gb_api_keep_pending(GB_Obj *errobj, F &&body) {
     return gb_api_impl<false>(errobj, std::forward<F>(body));
 }
 
+// ------------------------------------------------------------------ host-time probes
+// Diagnostics of the per-call host path (environment GRAPHBLAS_AMD_HPROF=1): cumulative
+// nanoseconds per named section, printed at exit.  A disabled probe costs one load.
+extern bool g_hprof_on;
+void gb_hprof_add(int slot, const char *name, int64_t ns);
+int64_t gb_hprof_now();
+struct gb_hprof_scope {
+    int slot;
+    const char *name;
+    int64_t t0;
+    gb_hprof_scope(int s, const char *n) : slot(s), name(n), t0(g_hprof_on ? gb_hprof_now() : 0) {}
+    ~gb_hprof_scope() {
+        if (g_hprof_on) gb_hprof_add(slot, name, gb_hprof_now() - t0);
+    }
+};
+#define GB_HPROF(slot, name) gb_hprof_scope gb_hprof_##slot(slot, name)
+
 // ------------------------------------------------------------------ context
 hipStream_t gb_stream();
 void gb_require_init();
@@ -281,7 +299,7 @@ struct gb_csr_view {
     const int32_t *hubs = nullptr;
     int64_t nhubs = 0, hub_H = 0;
     const uint64_t *nonempty = nullptr;  // bitmap of rows with entries (when attached)
-    const int32_t *pfirst = nullptr;     // hub-first probe per row (when attached; -1: empty row)
+    const int32_t *phead = nullptr;      // pull head per row, 4 int32 (when attached; see GB_Obj)
     const uint32_t *pdeg = nullptr;      // row length in the other orientation (when attached)
     const int32_t *lchunks = nullptr;    // long-row chunks (row, piece) of the general SpMV (when attached)
     int64_t nlchunks = -1;
@@ -300,8 +318,9 @@ void gb_get_csr(gb_csr_view &v, GB_Obj *A);
 void gb_view_hubs(gb_csr_view &v, GB_Obj *A, int orient, int64_t H);
 // attach the cached non-empty-rows bitmap of matrix A's orientation to v
 void gb_view_nonempty(gb_csr_view &v, GB_Obj *A, int orient);
-// attach the cached hub-first probes of A's orientation (other_rowptr: the other orientation's
-// row pointers, other_n rows) -- the iso pull tests a row's best-connected neighbour first
+// attach the cached pull heads of A's orientation (other_rowptr: the other orientation's row
+// pointers, other_n rows) -- the iso pull tests a row's best-connected neighbours first, and
+// rows of at most 4 entries without reading their bounds or edges
 void gb_view_pullfirst(gb_csr_view &v, GB_Obj *A, int orient, const int64_t *other_rowptr, int64_t other_n);
 void gb_view_long_rows(gb_csr_view &v, GB_Obj *A, int orient);
 // attach (building on first use) the column-sliced copy of matrix A's orientation

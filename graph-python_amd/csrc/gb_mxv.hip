@@ -432,7 +432,7 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
                                                       int p1_steps, int cap0, const uint64_t *__restrict__ rne,
                                                       const uint64_t *__restrict__ qbits, const gb_asg_dev &g,
                                                       long long &adelta, int dbg = 0,
-                                                      const int32_t *__restrict__ pf = nullptr,
+                                                      const int32_t *__restrict__ ph = nullptr,
                                                       const uint32_t *__restrict__ pdeg = nullptr) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -466,19 +466,28 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
             live[u] = (__shfl(mine, u, 64) >> lane) & 1ULL;
             found[u] = false;
         }
-        if (pf) {
-            // hub-first probe: each open row tests its best-connected neighbour (one coalesced
-            // 4-byte load per row); rows it settles never read their row bounds or edges
-            int32_t kf[PULL_U];
+        if (ph) {
+            // pull heads: each open row first tests its best-connected neighbours (one coalesced
+            // 16-byte load per row); rows they settle, and rows of at most 4 entries, never read
+            // their bounds or edges -- the dependent row-pointer / edge round trips are left to
+            // the long rows that found nothing
+            int4 hv[PULL_U];
 #pragma unroll
-            for (int u = 0; u < PULL_U; u++) kf[u] = live[u] ? pf[((w0 + u) << 6) + lane] : -1;
+            for (int u = 0; u < PULL_U; u++) {
+                hv[u] = make_int4(-1, -1, -1, -1);
+                if (live[u]) hv[u] = reinterpret_cast<const int4 *>(ph)[((w0 + u) << 6) + lane];
+            }
 #pragma unroll
-            for (int u = 0; u < PULL_U; u++) found[u] = kf[u] >= 0 && gb_bit(ubits, kf[u]);
+            for (int u = 0; u < PULL_U; u++)
+                found[u] = (hv[u].x >= 0 && gb_bit(ubits, hv[u].x)) ||
+                           (hv[u].y >= 0 && gb_bit(ubits, hv[u].y)) ||
+                           (hv[u].z >= 0 && gb_bit(ubits, hv[u].z)) ||
+                           (hv[u].w >= 0 && gb_bit(ubits, hv[u].w));
 #pragma unroll
             for (int u = 0; u < PULL_U; u++) {
                 const int64_t r = ((w0 + u) << 6) + lane;
                 p[u] = p1[u] = 0;
-                if (live[u] && !found[u] && r < nrows) {
+                if (live[u] && !found[u] && hv[u].w == -2 && r < nrows) {  // a long row: walk it
                     p[u] = rowptr[r];
                     p1[u] = rowptr[r + 1];
                 }
@@ -677,7 +686,7 @@ struct gb_iso_args {
                                     // 16 pull without its segment list, 32 pull steps without probes (wrong results)
     bool packed;                    // one-round finish (iso_finish_packed): n < 2^27
     const uint64_t *rows_nonempty;  // pull rows with entries (nullptr: all)
-    const int32_t *pfirst;          // hub-first probe per pull row (nullptr: none)
+    const int32_t *phead;           // pull head per row, 4 int32 (nullptr: none; gb_view_pullfirst)
     const uint32_t *pdeg;           // push-orientation length per pull row (the hint of found rows)
     // fused deferred assign (gb_asg): w<q>(:) = x with q = u (asg.bits nullptr: none)
     gb_asg_dev asg;
@@ -1172,7 +1181,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
     else
         cnt = gb_pull_iso_phase(nrows, rowptr, colidx, ubits, mbits, mcomp, tbits, L, a.hprow, mfn, a.p1_steps,
                                 a.cap0, a.rows_nonempty, qbits, a.asg, adelta, a.dbg,
-                                (a.pfirst && (!a.hprow || a.pdeg)) ? a.pfirst : nullptr, a.pdeg);
+                                (a.phead && (!a.hprow || a.pdeg)) ? a.phead : nullptr, a.pdeg);
     if (a.packed) {
         iso_finish_packed(cnt, mfn, adelta, tcount, gst, a);
         return;
@@ -1277,41 +1286,50 @@ void gb_view_nonempty(gb_csr_view &v, GB_Obj *A, int orient) {
     v.nonempty = A->rows_ne[orient];
 }
 
-// hub-first probes: a wave per row picks the neighbour with the longest row in the other
-// orientation (ties: the smaller index) -- in a level BFS that neighbour is the one most
-// likely to be in the frontier, so most rows the pull settles are settled by it -- and
+// pull heads: a wave per row picks its neighbours with the longest rows in the other
+// orientation (ties: the smaller index) -- in a level BFS those are the ones most likely to
+// be in the frontier, so most rows the pull settles are settled by them -- 3 of them for a
+// row longer than 4 (4th slot -2: "walk the row"), the whole row otherwise (padding -1), and
 // stores the row's own length in the other orientation (the next-frontier hint of a row
 // settled without reading its bounds)
-__global__ __launch_bounds__(256) void k_pull_first(int64_t n, const int64_t *__restrict__ rp,
-                                                    const int32_t *__restrict__ ci,
-                                                    const int64_t *__restrict__ orp, int64_t on,
-                                                    int32_t *__restrict__ pf, uint32_t *__restrict__ pdeg) {
+__device__ __forceinline__ void pf_better(int64_t &bd, int32_t &bi, int64_t d, int32_t i) {
+    if (i >= 0 && (d > bd || (d == bd && (bi < 0 || i < bi)))) {
+        bd = d;
+        bi = i;
+    }
+}
+__global__ __launch_bounds__(256) void k_pull_head(int64_t n, const int64_t *__restrict__ rp,
+                                                   const int32_t *__restrict__ ci,
+                                                   const int64_t *__restrict__ orp, int64_t on,
+                                                   int4 *__restrict__ head, uint32_t *__restrict__ pdeg) {
     const int lane = threadIdx.x & 63;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     for (int64_t j = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; j < n; j += nwaves) {
-        int64_t bd = -1;
-        int32_t bi = -1;
-        for (int64_t e = rp[j] + lane; e < rp[j + 1]; e += 64) {
-            const int32_t i = ci[e];
-            const int64_t d = orp[i + 1] - orp[i];
-            if (d > bd || (d == bd && i < bi)) {
-                bd = d;
-                bi = i;
+        const int64_t e0 = rp[j], e1 = rp[j + 1], d = e1 - e0;
+        int32_t pick[4] = {-1, -1, -1, -1};
+        const int rounds = d <= 4 ? (int)d : 3;
+        for (int r = 0; r < rounds; r++) {
+            int64_t bd = -1;
+            int32_t bi = -1;
+            for (int64_t e = e0 + lane; e < e1; e += 64) {
+                const int32_t i = ci[e];
+                bool taken = false;
+                for (int q = 0; q < r; q++) taken = taken || pick[q] == i;
+                if (!taken) pf_better(bd, bi, orp[i + 1] - orp[i], i);
             }
-        }
-        for (int off = 32; off > 0; off >>= 1) {
-            const int64_t od = __shfl_xor(bd, off, 64);
-            const int32_t oi = __shfl_xor(bi, off, 64);
-            if (od > bd || (od == bd && oi >= 0 && (bi < 0 || oi < bi))) {
-                bd = od;
-                bi = oi;
+            for (int off = 32; off > 0; off >>= 1) {
+                const int64_t od = __shfl_xor(bd, off, 64);
+                const int32_t oi = __shfl_xor(bi, off, 64);
+                pf_better(bd, bi, od, oi);
             }
+            pick[r] = bi;  // identical on every lane
         }
+        if (d > 4) pick[3] = -2;
         if (lane == 0) {
-            pf[j] = bi;
+            head[j] = make_int4(pick[0], pick[1], pick[2], pick[3]);
             if (pdeg) {
-                const int64_t d = j < on ? orp[j + 1] - orp[j] : 0;
-                pdeg[j] = (uint32_t)(d < 0xFFFFFFFFLL ? d : 0xFFFFFFFFLL);
+                const int64_t od = j < on ? orp[j + 1] - orp[j] : 0;
+                pdeg[j] = (uint32_t)(od < 0xFFFFFFFFLL ? od : 0xFFFFFFFFLL);
             }
         }
     }
@@ -1319,15 +1337,15 @@ __global__ __launch_bounds__(256) void k_pull_first(int64_t n, const int64_t *__
 
 void gb_view_pullfirst(gb_csr_view &v, GB_Obj *A, int orient, const int64_t *other_rowptr, int64_t other_n) {
     if (A->kind != GB_KIND_MATRIX || v.nrows == 0) return;
-    if (!A->pfirst[orient]) {
-        A->pfirst[orient] = gb_malloc_n<int32_t>(v.nrows);
+    if (!A->phead[orient]) {
+        A->phead[orient] = gb_malloc_n<int32_t>(4 * v.nrows);
         A->pdeg[orient] = gb_malloc_n<uint32_t>(v.nrows);
         const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((v.nrows + 3) / 4, 65535));
-        hipLaunchKernelGGL(k_pull_first, dim3(g), dim3(256), 0, gb_stream(), v.nrows, v.rowptr, v.colidx,
-                           other_rowptr, other_n, A->pfirst[orient], A->pdeg[orient]);
+        hipLaunchKernelGGL(k_pull_head, dim3(g), dim3(256), 0, gb_stream(), v.nrows, v.rowptr, v.colidx,
+                           other_rowptr, other_n, reinterpret_cast<int4 *>(A->phead[orient]), A->pdeg[orient]);
         GB_LAUNCH_CHECK();
     }
-    v.pfirst = A->pfirst[orient];
+    v.phead = A->phead[orient];
     v.pdeg = A->pdeg[orient];
 }
 
@@ -1432,7 +1450,7 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             args.cap0 = (int)gb_knob("pull_cap");
             if (args.cap0 <= 0) args.cap0 = 16;
             args.rows_nonempty = A.nonempty;
-            args.pfirst = A.pfirst;
+            args.phead = A.phead;
             args.pdeg = A.pdeg;
             // the result's iso value: evaluated by the finishing block when z is x's type or bool
             const bool eval_ok = info.zcode == info.xcode || info.zcode == GBAMD_T_BOOL;
@@ -1509,6 +1527,7 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             if (gcap <= 0) gcap = iso_work_resident_blocks();
             const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 3) / 4, gcap));
             if (grid >= GB_GRID_SHARDS * ((1u << ISO_ARR_BITS) - 1)) args.packed = false;  // arrival field
+            GB_HPROF(5, "k_iso_work launch");
             hipLaunchKernelGGL(k_iso_work, dim3(grid), dim3(SPMV_BLOCK), 0, gb_stream(), n, A.rowptr, A.colidx, uw,
                                u.bits, can_push ? Apush->rowptr : nullptr, can_push ? Apush->colidx : nullptr,
                                can_push ? Apush->hubs : nullptr, can_push ? Apush->nhubs : 0,

@@ -128,9 +128,9 @@ void gb_drop_transpose(GB_Obj *A) {
         A->hub_n[o] = A->hub_H[o] = 0;
         gb_free(A->rows_ne[o]);
         A->rows_ne[o] = nullptr;
-        gb_free(A->pfirst[o]);
+        gb_free(A->phead[o]);
         gb_free(A->pdeg[o]);
-        A->pfirst[o] = nullptr;
+        A->phead[o] = nullptr;
         A->pdeg[o] = nullptr;
         gb_free(A->long_tab[o]);
         A->long_tab[o] = nullptr;
@@ -1137,6 +1137,7 @@ GrB_Info GrB_Matrix_dup(GrB_Matrix *C, const GrB_Matrix A) {
     return gb_api(nullptr, [&] { *C = (GrB_Matrix)dup_object(gb_obj_check(A)); });
 }
 GrB_Info GrB_Matrix_clear(GrB_Matrix A) {
+    GB_HPROF(6, "GrB_*_clear");
     GB_Obj *o = OBJ(A);
     return gb_api(o, [&] {
         gb_obj_check_raw(A);
@@ -1154,6 +1155,7 @@ GrB_Info GrB_Matrix_ncols(GrB_Index *n, const GrB_Matrix A) {
 }
 GrB_Info GrB_Matrix_nvals(GrB_Index *n, const GrB_Matrix A) {
     if (!n) return GrB_NULL_POINTER;
+    GB_HPROF(7, "GrB_*_nvals (incl. wait)");
     return gb_api(OBJ(A), [&] { *n = gb_nvals(gb_obj_check_raw(A)); });
 }
 GrB_Info GrB_Matrix_resize(GrB_Matrix A, GrB_Index nrows, GrB_Index ncols) {

@@ -42,6 +42,7 @@ static bool take_pending_assign(gb_asg &asg, GB_Obj *w, GB_Obj *mask, GB_Obj *A,
 // ================================================================== mxv / vxm
 static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr, GB_Obj *A, GB_Obj *u,
                     const gb_desc &d, bool vxm) {
+    GB_HPROF(1, "do_spmv total");
     check_semiring(sr);
     check_binop(accum, true);
     // rows of the operand matrix the kernel pulls along:
@@ -60,6 +61,7 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
                 take_pending_assign(asg, w, mask, A, u, d, gb_spmv_result_iso(sr, A->iso, u->iso, vxm));
         if (!fused) gb_pending_flush();
     }
+    const int64_t hp_t0 = g_hprof_on ? gb_hprof_now() : 0;
     gb_csr_view av, pv;
     if (use_csc) gb_get_csc(av, A);
     else gb_get_csr(av, A);
@@ -90,14 +92,19 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
         push = &pv;
         if (gb_knob("pull_first") != 1) gb_view_pullfirst(av, A, use_csc ? 1 : 0, pv.rowptr, pv.nrows);
     }
+    if (g_hprof_on) gb_hprof_add(2, "do_spmv views+mask", gb_hprof_now() - hp_t0);
     gb_vec_result T;
     if (w->kind != GB_KIND_MATRIX) {
         if (!w->pub) w->pub = gb_host_slot_alloc();
         T.pub = w->pub;
         T.pub_seq = gb_next_pub_seq();
     }
-    gb_spmv(T, av, push, uv, m, sr, vxm, fused ? &asg : nullptr);
+    {
+        GB_HPROF(3, "gb_spmv (host+launch)");
+        gb_spmv(T, av, push, uv, m, sr, vxm, fused ? &asg : nullptr);
+    }
     const void *hint_key = T.hint_key;
+    GB_HPROF(4, "writeback+epilogue");
     const bool direct = gb_writeback_vector(w, T, mask, d, accum, true);
     if (direct && T.published) {
         // w's count is the one the kernel published; valid until more work is enqueued
@@ -936,6 +943,7 @@ GrB_Info GrB_mxv(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum, 
 
 GrB_Info GrB_vxm(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum, const GrB_Semiring op,
                  const GrB_Vector u, const GrB_Matrix A, const GrB_Descriptor desc) {
+    GB_HPROF(0, "GrB_vxm total");
     return gb_api_keep_pending(OBJ(w), [&] {
         do_spmv(gb_obj_check(w), gb_obj_check(mask, true), accum, op, gb_obj_check(A), gb_obj_check(u),
                 gb_read_desc(desc), true);

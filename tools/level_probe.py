@@ -73,4 +73,6 @@ print(f"root {src} (index {root_idx}), out-degree {deg[src]}")
 print(" lvl  frontier     auto_us     pull_us     push_us   next")
 for i in range(len(res[0])):
     d, f, ta, nx = res[0][i]
-    print(f"{d:4d} {f:9d} {ta:11.1f} {res[1][i][2]:11.1f} {res[2][i][2]:11.1f} {nx:7d}")
+    tp = res[1][i][2] if i < len(res[1]) else float("nan")  # diagnostic knobs may change the levels
+    tu = res[2][i][2] if i < len(res[2]) else float("nan")
+    print(f"{d:4d} {f:9d} {ta:11.1f} {tp:11.1f} {tu:11.1f} {nx:7d}")
