@@ -1444,8 +1444,9 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             args.dbg = (int)gb_knob("iso_dbg");
             args.packed = n < (1LL << ISO_VAL_BITS) && u.n < (1LL << ISO_VAL_BITS) && gb_knob("iso_packed") != 1;
             if (args.dbg & 1) T.pub = nullptr;  // diagnostics: the host reads the count by a copy
-            args.p1_steps = (int)gb_knob("pull_steps");  // -1: no lane-per-row steps
-            if (args.p1_steps == 0) args.p1_steps = 2;
+            // lane-per-row steps after the pull heads: none by default (tools/gpu_ab2.sh, s22
+            // any_pair: 0.340 ms/BFS without, 0.356 with 2, 0.350 with 1)
+            args.p1_steps = (int)gb_knob("pull_steps");
             if (args.p1_steps < 0) args.p1_steps = 0;
             args.cap0 = (int)gb_knob("pull_cap");
             if (args.cap0 <= 0) args.cap0 = 16;
