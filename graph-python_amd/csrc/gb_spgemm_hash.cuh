@@ -419,6 +419,9 @@ __global__ __launch_bounds__(BS) void k_hash_block(
             if (tid == BS - 1) s_excl[BS] = wbase + inc;
             __syncthreads();
             const int64_t G = s_excl[BS];
+            const int ne = a1 - g < BS ? (int)(a1 - g) : BS;  // entries of this group
+            int top = 1;
+            while (top < ne) top <<= 1;
             for (int64_t t0 = 0; t0 < G; t0 += TILE) {
                 int sx[P];
                 int64_t pb[P];
@@ -429,9 +432,8 @@ __global__ __launch_bounds__(BS) void k_hash_block(
                     ok[u] = t < G;
                     int s = 0;
                     if (ok[u]) {
-#pragma unroll
-                        for (int st = BS / 2; st > 0; st >>= 1)
-                            if (s_excl[s + st] <= t) s += st;
+                        for (int st = top >> 1; st > 0; st >>= 1)
+                            if (s + st < ne && s_excl[s + st] <= t) s += st;
                     }
                     sx[u] = s;
                     pb[u] = ok[u] ? s_b0[s] + (t - s_excl[s]) : 0;
@@ -655,11 +657,13 @@ __device__ __forceinline__ int32_t win_advance(const win_sweep_lds &L, int64_t g
 }
 
 template <class F>
-__device__ __forceinline__ void win_tiles(const win_sweep_lds &L, int64_t g, int32_t c0,
+__device__ __forceinline__ void win_tiles(const win_sweep_lds &L, int64_t g, int ne, int32_t c0,
                                           const int32_t *__restrict__ bci, F &&f) {
     constexpr int TILE = HG * WP;
     const int tid = threadIdx.x;
     const int32_t G = L.excl[WEG];
+    int top = 1;  // the search covers entries [0, ne): the last entry with excl <= t is below ne
+    while (top < ne) top <<= 1;
     for (int32_t t0 = 0; t0 < G; t0 += TILE) {
         int sx[WP];
         int64_t pb[WP];
@@ -671,8 +675,8 @@ __device__ __forceinline__ void win_tiles(const win_sweep_lds &L, int64_t g, int
             int s = 0;
             if (ok[u]) {
 #pragma unroll
-                for (int st = WEG / 2; st > 0; st >>= 1)
-                    if (L.excl[s + st] <= t) s += st;
+                for (int st = top >> 1; st > 0; st >>= 1)
+                    if (s + st < ne && L.excl[s + st] <= t) s += st;
             }
             sx[u] = s;
             pb[u] = ok[u] ? L.lo[s] + (t - L.excl[s]) : 0;
@@ -698,7 +702,7 @@ __device__ __forceinline__ int32_t win_sweep(win_sweep_lds &L, int64_t a0, int64
             const int32_t m = win_advance(L, g, ne, cur, bci);
             mn = m < mn ? m : mn;
         }
-        win_tiles(L, g, c0, bci, f);
+        win_tiles(L, g, ne, c0, bci, f);
         __syncthreads();
     }
     return mn;
@@ -711,7 +715,7 @@ __global__ __launch_bounds__(HG) void k_row_window(
     SR sr, const int32_t *__restrict__ rows, int64_t nr, int logW, int64_t *__restrict__ cur,
     const int64_t *__restrict__ arp, const int32_t *__restrict__ aci, const int64_t *__restrict__ brp,
     const int32_t *__restrict__ bci, int64_t ncols, int64_t *__restrict__ cnt, const int64_t *__restrict__ crp,
-    int32_t *__restrict__ cci) {
+    int32_t *__restrict__ cci, uint32_t *__restrict__ rowbits, int64_t nwrow, int32_t *__restrict__ bslot) {
     constexpr int NW = HG / 64;
     extern __shared__ __align__(16) char smem[];
     const int W = 1 << logW;        // columns per window (multiple of 256)
@@ -747,9 +751,12 @@ __global__ __launch_bounds__(HG) void k_row_window(
             cur[p] = b0;
             if (b0 < brp[k + 1]) nmin = bci[b0] < nmin ? bci[b0] : nmin;
         }
-        int32_t c0 = block_min(nmin);
+        // windows start at multiples of 32 columns (bitmap words line up with the stored row bitmap)
+        int32_t c0 = block_min(nmin) & ~31;
         int64_t count = 0;
         int64_t outpos = SYM ? 0 : crp[i];
+        uint32_t *rb = (SYM && rowbits) ? rowbits + r * nwrow : nullptr;  // this row's stored bitmap (zeroed)
+        if (rb && tid == 0) bslot[i] = (int32_t)r;
         while (c0 < ncols) {
             const int64_t c1 = (int64_t)c0 + W;
             for (int q = tid; q < NWD; q += HG) bm[q] = 0u;
@@ -784,20 +791,21 @@ __global__ __launch_bounds__(HG) void k_row_window(
             }
             if constexpr (SYM) {
                 count += m;
+                if (rb) {  // the window's presence bits, for the numeric pass (k_window_num)
+                    const int64_t w0 = c0 >> 5;
+                    for (int q = tid; q < NWD && w0 + q < nwrow; q += HG) rb[w0 + q] = bm[q];
+                }
             } else {
                 for (int q = q0; q < q1; q++) {
-                    prew[q] = run;
-                    run += __popc(bm[q]);
-                }
-                __syncthreads();
-                for (int q = w * 2; q < NWD; q += NW * 2) {
-                    const uint64_t bits = (uint64_t)bm[q] | ((uint64_t)bm[q + 1] << 32);
-                    if ((bits >> lane) & 1ULL)
-                        cci[outpos + prew[q] + __popcll(bits & ((1ULL << lane) - 1))] = c0 + q * 32 + lane;
+                    uint32_t bits = bm[q];
+                    while (bits) {
+                        cci[outpos + run++] = c0 + q * 32 + __builtin_ctz(bits);
+                        bits &= bits - 1u;
+                    }
                 }
                 outpos += m;
             }
-            c0 = block_min(mn);
+            c0 = block_min(mn) & ~31;
         }
         if constexpr (SYM) {
             if (tid == 0) cnt[i] = count;
@@ -817,7 +825,8 @@ __global__ __launch_bounds__(HG) void k_window_num(
     int64_t *__restrict__ cur, const int64_t *__restrict__ arp, const int32_t *__restrict__ aci,
     const X *__restrict__ avx, bool a_iso, const int64_t *__restrict__ brp, const int32_t *__restrict__ bci,
     const X *__restrict__ bvx, bool b_iso, int64_t ncols, const int64_t *__restrict__ crp,
-    int32_t *__restrict__ cci, Z *__restrict__ cvx) {
+    int32_t *__restrict__ cci, Z *__restrict__ cvx, const uint32_t *__restrict__ rowbits, int64_t nwrow,
+    const int32_t *__restrict__ bslot) {
     using S = slot_of<Z>;
     constexpr int NW = HG / 64, TILE = HG * WP;
     extern __shared__ __align__(16) char smem[];
@@ -867,11 +876,19 @@ __global__ __launch_bounds__(HG) void k_window_num(
             cur[p] = b0;
             if (b0 < brp[k + 1]) nmin = bci[b0] < nmin ? bci[b0] : nmin;
         }
-        int32_t c0 = block_min(nmin);
+        int32_t c0 = block_min(nmin) & ~31;
         int64_t outpos = crp[i];
+        // the row's presence bits from the symbolic pass (k_row_window), when it stored them
+        const int32_t slot = rowbits ? bslot[i] : -1;
+        const uint32_t *rb = slot >= 0 ? rowbits + (int64_t)slot * nwrow : nullptr;
         while (c0 < ncols) {
             const int64_t c1 = (int64_t)c0 + W;
-            for (int q = tid; q < NWD; q += HG) bm[q] = 0u;
+            if (rb) {
+                const int64_t w0 = c0 >> 5;
+                for (int q = tid; q < NWD; q += HG) bm[q] = w0 + q < nwrow ? rb[w0 + q] : 0u;
+            } else {
+                for (int q = tid; q < NWD; q += HG) bm[q] = 0u;
+            }
             __syncthreads();
             auto presence = [&](const bool(&ok)[WP], const int32_t(&c)[WP], const int64_t(&)[WP], const int(&)[WP],
                                 int64_t) {
@@ -881,11 +898,11 @@ __global__ __launch_bounds__(HG) void k_window_num(
             };
             // a row of one entry group keeps its entry tables in LDS from the presence sweep to a
             // value sweep over the whole window (one group, or C-resident)
-            const bool one = a1 - a0 <= WEG;
+            const bool one = !rb && a1 - a0 <= WEG;
             if (one) {
                 win_entries(L, a0, (int)(a1 - a0), c1, cur, aci, brp, bci);
-                win_tiles(L, a0, c0, bci, presence);
-            } else {
+                win_tiles(L, a0, (int)(a1 - a0), c0, bci, presence);
+            } else if (!rb) {
                 win_sweep(L, a0, a1, c0, c1, false, cur, aci, brp, bci, presence);
             }
             __syncthreads();
@@ -909,17 +926,16 @@ __global__ __launch_bounds__(HG) void k_window_num(
                 if (q < w) run += (int32_t)s_wsum[q];
                 m += s_wsum[q];
             }
+            // sorted columns of the window: each thread writes the set bits of its own words
             for (int q = q0; q < q1; q++) {
                 prew[q] = run;
-                run += __popc(bm[q]);
+                uint32_t bits = bm[q];
+                while (bits) {
+                    cci[outpos + run++] = c0 + q * 32 + __builtin_ctz(bits);
+                    bits &= bits - 1u;
+                }
             }
             __syncthreads();
-            // sorted columns of the window: a wave per 64-column stretch, ballot + prefix
-            for (int q = w * 2; q < NWD; q += NW * 2) {
-                const uint64_t bits = (uint64_t)bm[q] | ((uint64_t)bm[q + 1] << 32);
-                if ((bits >> lane) & 1ULL)
-                    cci[outpos + prew[q] + __popcll(bits & ((1ULL << lane) - 1))] = c0 + q * 32 + lane;
-            }
             // values of the products in [cursor, cend) into dst[rank - rbase], owner slices of
             // 2^osh slots; the cursors advance to cend
             // whole: the sweep covers the window from its start (one group, or C-resident)
@@ -970,7 +986,7 @@ __global__ __launch_bounds__(HG) void k_window_num(
                         }
                 };
                 if (one && whole) {  // entry tables still in LDS from the presence sweep
-                    win_tiles(L, a0, c0, bci, f);
+                    win_tiles(L, a0, (int)(a1 - a0), c0, bci, f);
                     __syncthreads();
                     return win_advance(L, a0, (int)(a1 - a0), cur, bci);
                 }
@@ -1015,7 +1031,7 @@ __global__ __launch_bounds__(HG) void k_window_num(
                 }
             }
             outpos += m;
-            c0 = block_min(mn);
+            c0 = block_min(mn) & ~31;
         }
         __syncthreads();
     }
@@ -1188,6 +1204,9 @@ void spgemm_hash_run(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, const gb_
     // one phase over the bins; SYM counts into cnt, else writes rows: hash bins into (hci, hvx),
     // window rows (already in column order) into (wci, wvx)
     const int64_t *hrow = nullptr;  // row offsets of the hash bins' scratch (numeric)
+    uint32_t *rowbits = nullptr;    // window rows' presence bitmaps (symbolic -> numeric)
+    int32_t *bslot = nullptr;       // per row: its bitmap's slot, -1 none
+    int64_t nwrow = 0;              // words per row bitmap
     auto phase = [&](auto symc, auto valsc, const bins_t &b, int32_t *hci, Z *hvx, int32_t *wci, Z *wvx) {
         constexpr bool SYM = decltype(symc)::value;
         constexpr bool VALS = decltype(valsc)::value;
@@ -1259,7 +1278,7 @@ void spgemm_hash_run(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, const gb_
                     hipLaunchKernelGGL((k_window_num<D, SRT, X, Z>), dim3(hgrid(b.c[4], 1, 2048)), dim3(HG), sh,
                                        gb_stream(), srf, mon, rows + b.st[4], b.c[4], lw, vcap, in_c_groups, cur,
                                        A.rowptr, A.colidx, ax, A.iso, B.rowptr, B.colidx, bx, B.iso, ncols, crp,
-                                       wci, wvx);
+                                       wci, wvx, (const uint32_t *)rowbits, nwrow, (const int32_t *)bslot);
                 };
                 if constexpr (FP) {
                     if (det) win(std::true_type{});
@@ -1272,7 +1291,8 @@ void spgemm_hash_run(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, const gb_
                 set_lds(k_row_window<SYM, SRT, X, Z>, sh);
                 hipLaunchKernelGGL((k_row_window<SYM, SRT, X, Z>), dim3(hgrid(b.c[4], 1, 2048)), dim3(HG), sh,
                                    gb_stream(), srf, rows + b.st[4], b.c[4], lw, cur, A.rowptr, A.colidx,
-                                   B.rowptr, B.colidx, ncols, cnt, crp, wci);
+                                   B.rowptr, B.colidx, ncols, cnt, crp, wci, SYM ? rowbits : nullptr, nwrow,
+                                   SYM ? bslot : nullptr);
             }
         }
         GB_LAUNCH_CHECK();
@@ -1280,6 +1300,22 @@ void spgemm_hash_run(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, const gb_
 
     // ---- symbolic: bin by min(flops, ncols) against the key-only table capacities
     bins_t bs = make_bins(flops, TW_SYM / 2, TB_SYM / 2, TL_SYM / 2);
+    // the window rows' presence bitmaps (n bits each) are kept from the symbolic pass for the
+    // numeric one, which then skips its presence sweep -- when they take at most a quarter of
+    // the free device memory (knob window_bits=1: never)
+    gb_scratch rbs;
+    if (bs.c[4] && gb_knob("window_bits") != 1) {
+        const int64_t nw = (ncols + 31) / 32;
+        const size_t bytes = (size_t)bs.c[4] * (size_t)nw * 4;
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess && bytes <= fr / 4) {
+            rowbits = rbs.get<uint32_t>((size_t)bs.c[4] * (size_t)nw);
+            bslot = rbs.get<int32_t>(nrows);
+            nwrow = nw;
+            gb_memset(rowbits, 0, bytes);
+            gb_memset(bslot, 0xff, (size_t)nrows * sizeof(int32_t));
+        }
+    }
     phase(std::true_type{}, std::false_type{}, bs, (int32_t *)nullptr, (Z *)nullptr, (int32_t *)nullptr,
           (Z *)nullptr);
     gb_exclusive_scan_i64(cnt, T.rowptr, nrows);

@@ -40,6 +40,7 @@ def _knobs(gb, **kv):
 METHODS = {
     "bins": {},  # wave / workgroup tables for most rows, windows for the hubs
     "window": {"hash_window": 1},  # every row through the column windows (LDS value groups)
+    "window_sweep": {"hash_window": 1, "window_bits": 1},  # presence by a product sweep, not stored bitmaps
     "window_in_c": {"hash_window": 1, "window_vcap": 512, "window_in_c_groups": 1},
 }
 

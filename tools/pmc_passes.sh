@@ -12,7 +12,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${name}_trace" -o run -- "$@" \
   > "$R/gpurun_out/${name}_trace.log" 2>&1 || { tail -20 "$R/gpurun_out/${name}_trace.log"; exit 1; }
 i=0
-for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_VALU"; do
+for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_VALU" ${PMC_EXTRA:+"$PMC_EXTRA"}; do
   i=$((i+1))
   timeout -s KILL 180 rocprofv3 --kernel-include-regex "$regex" --pmc $set --output-format csv \
     -d "$R/gpurun_out/${name}_pmc$i" -o run -- "$@" > "$R/gpurun_out/${name}_pmc$i.log" 2>&1 \
