@@ -1,3 +1,4 @@
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 // gb_context.cpp -- library context: init/finalize, the HIP stream, the
@@ -156,15 +157,21 @@ namespace {
 struct hprof_slot {
     std::atomic<int64_t> ns{0}, calls{0};
     const char *name = nullptr;
+    std::mutex mu;
+    std::vector<int64_t> samples;  // the first 1M durations (median / p10 at exit)
 };
 hprof_slot g_hprof[32];
 struct hprof_print {
     ~hprof_print() {
         if (!g_hprof_on) return;
         for (auto &s : g_hprof)
-            if (s.name && s.calls.load())
-                fprintf(stderr, "[hprof] %-28s calls %9lld  mean %8.2f us\n", s.name, (long long)s.calls.load(),
-                        s.ns.load() / 1e3 / (double)s.calls.load());
+            if (s.name && s.calls.load()) {
+                std::vector<int64_t> v = s.samples;
+                std::sort(v.begin(), v.end());
+                const double med = v.empty() ? 0.0 : v[v.size() / 2] / 1e3, p10 = v.empty() ? 0.0 : v[v.size() / 10] / 1e3;
+                fprintf(stderr, "[hprof] %-28s calls %9lld  mean %8.2f us  median %8.2f  p10 %8.2f\n", s.name,
+                        (long long)s.calls.load(), s.ns.load() / 1e3 / (double)s.calls.load(), med, p10);
+            }
     }
 } g_hprof_print;
 }  // namespace
@@ -176,6 +183,8 @@ void gb_hprof_add(int slot, const char *name, int64_t ns) {
     g_hprof[slot].name = name;
     g_hprof[slot].ns += ns;
     g_hprof[slot].calls += 1;
+    std::lock_guard<std::mutex> lk(g_hprof[slot].mu);
+    if (g_hprof[slot].samples.size() < (1u << 20)) g_hprof[slot].samples.push_back(ns);
 }
 
 int64_t gb_knob(const char *key) {

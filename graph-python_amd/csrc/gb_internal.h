@@ -101,6 +101,7 @@ struct GB_Matrix_opaque {
     // the row's own length in the other orientation (saturated to 32 bits)
     int32_t *phead[2];
     uint32_t *pdeg[2];
+    int64_t maxdeg[2];   // longest row of each orientation (host), built with the hub tables; -1 unknown
     // cached long-row chunk tables (general SpMV, gb_mxv.hip)
     int32_t *long_tab[2];
     int64_t long_n[2];
@@ -301,6 +302,7 @@ struct gb_csr_view {
     const uint64_t *nonempty = nullptr;  // bitmap of rows with entries (when attached)
     const int32_t *phead = nullptr;      // pull head per row, 4 int32 (when attached; see GB_Obj)
     const uint32_t *pdeg = nullptr;      // row length in the other orientation (when attached)
+    int64_t maxdeg = -1;                 // longest row (host; attached with the hub chunks, -1 unknown)
     const int32_t *lchunks = nullptr;    // long-row chunks (row, piece) of the general SpMV (when attached)
     int64_t nlchunks = -1;
     // column-sliced copy (when attached): 8 slice CSRs, int32 row pointers [8][nrows+1]
@@ -343,6 +345,7 @@ struct gb_bitmap_view {
     const long long *mf_hint = nullptr;  // device edge count of the entries (see GB_Obj::hint_key)
     const void *hint_key = nullptr;
     bool full = false;                   // every entry present, known on the host
+    int64_t h_nvals = -1;                // entries, when known on the host (-1: not known)
     gb_scratch own;
 };
 void gb_get_bitmap(gb_bitmap_view &v, GB_Obj *A);
@@ -404,6 +407,7 @@ struct gb_vmask {
     const uint64_t *bits = nullptr;  // nullptr: no mask
     bool comp = false;
     const int64_t *count = nullptr;  // device count of set mask bits, when known
+    int64_t h_count = -1;            // the same count known on the host (-1: not known)
     // value mask of an iso vector, left unmaterialised (only when the caller allows it):
     // the mask is `bits` if the device value *iso_val is nonzero, else empty
     const void *iso_val = nullptr;
@@ -475,6 +479,12 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
 bool gb_spmv_result_iso(GrB_Semiring sr, bool a_iso, bool u_iso, bool flip);
 void gb_spgemm(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, gb_csr_view *BT,
                gb_mmask &mask, GrB_Semiring sr);
+// Vector clears without a launch (gb_mxv.hip): a cleared vector takes a pre-zeroed bitmap and
+// count from a small pool; its old bitmap is zeroed by the next iso SpMV launch and returns to
+// the pool.  Returns false (nothing changed but the old bitmap possibly taken) when the pool
+// has nothing of this size: the caller then allocates and zeroes as usual.
+bool gb_zpool_clear_vector(GB_Obj *v);
+
 // hash Gustavson C = A*B (gb_spgemm_hash.hip): flops = per-row product counts
 void gb_spgemm_hash(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, GrB_Semiring sr, bool iso,
                     const void *av, const void *bv, const int64_t *flops);

@@ -660,6 +660,8 @@ __device__ void gb_iso_eval(int mul, int xcode, int zcode, bool flip, const void
     }
 }
 
+#define GB_ZP_MAX 4  // pooled cleared-vector storages zeroed per iso SpMV launch
+
 struct gb_iso_args {
     // direction: from the frontier's edge-count hint (the vector's producer
     // computed it), else from k_dir_prep's decision, else pull
@@ -688,6 +690,13 @@ struct gb_iso_args {
     const uint64_t *rows_nonempty;  // pull rows with entries (nullptr: all)
     const int32_t *phead;           // pull head per row, 4 int32 (nullptr: none; gb_view_pullfirst)
     const uint32_t *pdeg;           // push-orientation length per pull row (the hint of found rows)
+    int host_dir;                   // 1: push, decided on the host (small frontier of known size)
+    // storage of cleared vectors zeroed by this launch (gb_zpool_*): bitmaps of zb_words words,
+    // counts of 2 + GB_HINT_PARTS words
+    uint64_t *zb[GB_ZP_MAX];
+    int64_t *zc[GB_ZP_MAX];
+    int nzb, nzc;
+    int64_t zb_words;
     // fused deferred assign (gb_asg): w<q>(:) = x with q = u (asg.bits nullptr: none)
     gb_asg_dev asg;
     const void *asg_qiso;
@@ -1158,7 +1167,9 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
     gb_wlist &L = lists[threadIdx.x >> 6];
     if (a.dbg & 8) return;  // diagnostics: the launch alone
     bool push = false;
-    if (a.mf_hint) {
+    if (a.host_dir == 1) {
+        push = true;
+    } else if (a.mf_hint) {
         long long mf = 0;  // the hint's parts (one per grid-sum shard of its producer)
         for (int i = 0; i < GB_HINT_PARTS; i++) mf += a.mf_hint[i];
         push = gb_dir_decide(mf, a.rule);
@@ -1169,6 +1180,13 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
              w += (int64_t)gridDim.x * blockDim.x)
             a.spare[w] = 0;
     }
+    for (int j = 0; j < a.nzb; j++)  // cleared vectors' bitmaps, back to the pool zeroed
+        for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < a.zb_words;
+             w += (int64_t)gridDim.x * blockDim.x)
+            a.zb[j][w] = 0;
+    if (blockIdx.x == 0)
+        for (int j = 0; j < a.nzc; j++)
+            for (int w = threadIdx.x; w < 2 + GB_HINT_PARTS; w += blockDim.x) a.zc[j][w] = 0;
     // fused assign: q's value mask is empty when q is iso with a false value
     const uint64_t *qbits = nullptr;
     if (a.asg.bits && (!a.asg_qiso || gb_dyn_nonzero(a.asg_qiso, a.asg_qiso_code))) qbits = ubits;
@@ -1243,16 +1261,40 @@ static int32_t *gb_build_chunk_table(const gb_csr_view &v, int64_t thresh, int64
     return tab;
 }
 
+__global__ void k_row_maxlen(const int64_t *__restrict__ rowptr, int64_t n, unsigned long long *__restrict__ mx) {
+    unsigned long long m = 0;
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        const unsigned long long d = (unsigned long long)(rowptr[r + 1] - rowptr[r]);
+        m = d > m ? d : m;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(m, off, 64);
+        m = o > m ? o : m;
+    }
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(mx, m);
+}
+
 void gb_view_hubs(gb_csr_view &v, GB_Obj *A, int orient, int64_t H) {
     if (A->kind != GB_KIND_MATRIX) return;
     if (!A->hub_tab[orient] || A->hub_H[orient] != H) {
         gb_free(A->hub_tab[orient]);
         A->hub_tab[orient] = gb_build_chunk_table(v, H, H, &A->hub_n[orient]);
         A->hub_H[orient] = H;
+        // the longest row, for host-side direction decisions on small frontiers (gb_spmv)
+        gb_scratch s;
+        unsigned long long *mx = s.get<unsigned long long>(1);
+        gb_memset(mx, 0, sizeof(unsigned long long));
+        const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((v.nrows + 255) / 256, 2048));
+        hipLaunchKernelGGL(k_row_maxlen, dim3(g), dim3(256), 0, gb_stream(), v.rowptr, v.nrows, mx);
+        GB_LAUNCH_CHECK();
+        unsigned long long h = 0;
+        gb_copy_d2h(&h, mx, sizeof(h));
+        A->maxdeg[orient] = (int64_t)h + 1;  // stored + 1: 0 means not built
     }
     v.hubs = A->hub_tab[orient];
     v.nhubs = A->hub_n[orient];
     v.hub_H = H;
+    v.maxdeg = A->maxdeg[orient] - 1;
 }
 
 void gb_view_long_rows(gb_csr_view &v, GB_Obj *A, int orient) {
@@ -1364,6 +1406,45 @@ static bool idempotent_monoid(int m) {
 static std::mutex g_dir_mu;
 static uint64_t *g_spare = nullptr;  // zeroed bitmap for the next iso SpMV's output (under g_dir_mu)
 static int64_t g_spare_words = 0;
+
+// ---- pool of zeroed vector storage (under g_dir_mu): bitmaps of one size (g_zp_words) and
+// counts; `dirty` ones are zeroed by the next k_iso_work launch, then become `ready`
+static std::vector<uint64_t *> g_zp_ready_b, g_zp_dirty_b;
+static std::vector<int64_t *> g_zp_ready_c, g_zp_dirty_c;
+static int64_t g_zp_words = 0;
+
+bool gb_zpool_clear_vector(GB_Obj *v) {
+    if (gb_knob("zero_pool") == 1) return false;
+    std::lock_guard<std::mutex> lk(g_dir_mu);
+    const int64_t nw = gb_words(v->nrows);
+    if (nw != g_zp_words) {  // a new size: the pool follows the most recent one
+        for (auto *p : g_zp_ready_b) gb_free(p);
+        for (auto *p : g_zp_dirty_b) gb_free(p);
+        g_zp_ready_b.clear();
+        g_zp_dirty_b.clear();
+        g_zp_words = nw;
+    }
+    if (v->bits && (int)g_zp_dirty_b.size() < GB_ZP_MAX) {  // the old bitmap, to be zeroed later
+        g_zp_dirty_b.push_back(v->bits);
+        v->bits = nullptr;
+    }
+    if (g_zp_ready_b.empty() || g_zp_ready_c.empty()) return false;
+    gb_cw_release(v);
+    gb_free(v->bits);
+    gb_free(v->dense);
+    gb_free(v->d_nvals);
+    v->bits = g_zp_ready_b.back();
+    g_zp_ready_b.pop_back();
+    v->d_nvals = g_zp_ready_c.back();
+    g_zp_ready_c.pop_back();
+    v->dense = nullptr;
+    v->iso = false;
+    v->nvals = 0;
+    v->nvals_valid = true;
+    v->hint_valid = false;
+    v->pub_seq = 0;
+    return true;
+}
 
 // blocks of k_iso_work the device holds at once (the work grid is sized to one wave of blocks)
 static int64_t iso_work_resident_blocks() {
@@ -1486,8 +1567,26 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
                     T.hint_key = Apush->rowptr;
                 }
                 const bool hint_ok = u.mf_hint && u.hint_key == Apush->rowptr;
+                // no hint (a frontier set by the host, e.g. a BFS root): push is certain when even
+                // every frontier vertex having the longest row stays under the pull's least work
+                bool push_sure = false;
+                if (!hint_ok && spare_taken && eval_ok && u.h_nvals >= 0 && Apush->maxdeg >= 0 &&
+                    gb_knob("host_dir") != 1) {
+                    int64_t open_lo = -1;
+                    if (!mask.bits) {
+                        open_lo = n;
+                    } else if (mask.h_count >= 0) {
+                        const int64_t mc_hi = std::min<int64_t>(n, mask.h_count + (asg ? u.h_nvals : 0));
+                        open_lo = mask.comp ? n - mc_hi : mask.h_count;
+                    }
+                    const double avg = n ? (double)A.nvals / (double)n : 0.0;
+                    push_sure = open_lo >= 0 &&
+                                (double)u.h_nvals * (double)Apush->maxdeg * (double)alpha < (double)open_lo * avg;
+                }
                 if (hint_ok && spare_taken) {
                     args.mf_hint = u.mf_hint;  // decide in the work kernel: one launch
+                } else if (push_sure) {
+                    args.host_dir = 1;  // one launch, no prep
                 } else {
                     need_prep = true;
                 }
@@ -1524,6 +1623,14 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
                 args.spare = gb_malloc_n<uint64_t>(nw);
                 args.spare_words = nw;
             }
+            // cleared vectors' storage (gb_zpool_clear_vector): zeroed by this launch, then ready
+            while ((int)(g_zp_ready_c.size() + g_zp_dirty_c.size()) < GB_ZP_MAX)
+                g_zp_dirty_c.push_back(gb_malloc_n<int64_t>(2 + GB_HINT_PARTS));
+            args.nzb = (int)std::min<size_t>(g_zp_dirty_b.size(), GB_ZP_MAX);
+            for (int j = 0; j < args.nzb; j++) args.zb[j] = g_zp_dirty_b[j];
+            args.zb_words = g_zp_words;
+            args.nzc = (int)std::min<size_t>(g_zp_dirty_c.size(), GB_ZP_MAX);
+            for (int j = 0; j < args.nzc; j++) args.zc[j] = g_zp_dirty_c[j];
             int64_t gcap = gb_knob("iso_work_grid");
             if (gcap <= 0) gcap = iso_work_resident_blocks();
             const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 3) / 4, gcap));
@@ -1537,6 +1644,10 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             GB_LAUNCH_CHECK();
             g_spare = args.spare;
             g_spare_words = args.spare ? nw : 0;
+            for (int j = 0; j < args.nzb; j++) g_zp_ready_b.push_back(args.zb[j]);
+            g_zp_dirty_b.erase(g_zp_dirty_b.begin(), g_zp_dirty_b.begin() + args.nzb);
+            for (int j = 0; j < args.nzc; j++) g_zp_ready_c.push_back(args.zc[j]);
+            g_zp_dirty_c.erase(g_zp_dirty_c.begin(), g_zp_dirty_c.begin() + args.nzc);
             T.published = T.pub != nullptr;
             return;
         }

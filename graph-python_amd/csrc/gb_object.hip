@@ -126,6 +126,7 @@ void gb_drop_transpose(GB_Obj *A) {
         gb_free(A->hub_tab[o]);
         A->hub_tab[o] = nullptr;
         A->hub_n[o] = A->hub_H[o] = 0;
+        A->maxdeg[o] = 0;
         gb_free(A->rows_ne[o]);
         A->rows_ne[o] = nullptr;
         gb_free(A->phead[o]);
@@ -809,10 +810,13 @@ static void vector_set_element(GB_Obj *v, T x, int64_t i) {
             }
         }
     }
+    const bool was_empty = v->nvals_valid && v->nvals == 0;
     hipLaunchKernelGGL(k_vec_set<T>, dim3(1), dim3(1), 0, gb_stream(), (unsigned long long *)v->bits,
                        v->iso ? nullptr : (T *)v->dense, i, x, (unsigned long long *)v->d_nvals, iso_init);
     GB_LAUNCH_CHECK();
-    v->nvals_valid = false;
+    // the count stays known on the host when the vector was known to be empty
+    v->nvals_valid = was_empty;
+    v->nvals = was_empty ? 1 : v->nvals;
     v->hint_valid = false;
 }
 
@@ -1141,6 +1145,7 @@ GrB_Info GrB_Matrix_clear(GrB_Matrix A) {
     GB_Obj *o = OBJ(A);
     return gb_api(o, [&] {
         gb_obj_check_raw(A);
+        if (o->kind != GB_KIND_MATRIX && gb_zpool_clear_vector(o)) return;  // no launch
         gb_obj_free_storage(o);
         alloc_empty_storage(o);
     });
@@ -1384,6 +1389,7 @@ GrB_Info GrB_Scalar_error(const char **error, const GrB_Scalar s) {
         });                                                                                                  \
     }                                                                                                        \
     GrB_Info GrB_Vector_setElement_##T(GrB_Vector w, ctype x, GrB_Index i) {                                 \
+        GB_HPROF(9, "GrB_Vector_setElement");                                                                \
         return GrB_Matrix_setElement_##T((GrB_Matrix)w, x, i, 0);                                           \
     }                                                                                                        \
     GrB_Info GrB_Vector_extractElement_##T(ctype *x, const GrB_Vector v, GrB_Index i) {                      \

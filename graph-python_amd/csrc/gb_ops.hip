@@ -72,8 +72,11 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
         uv.mf_hint = (const long long *)(u->d_nvals + 2);  // GB_HINT_PARTS parts
         uv.hint_key = u->hint_key;
     }
+    if (u->kind != GB_KIND_MATRIX && u->nvals_valid) uv.h_nvals = u->nvals;
     gb_vmask m;
     gb_make_vmask(m, mask, d, a_rows);
+    // an empty mask vector: its count is known on the host (value or structure alike)
+    if (m.bits && mask && mask->kind != GB_KIND_MATRIX && mask->nvals_valid && mask->nvals == 0) m.h_count = 0;
     // the other orientation (cached on matrices) enables the push direction for iso results
     const gb_csr_view *push = nullptr;
     const bool iso_result = gb_spmv_result_iso(sr, A->iso, uv.iso, vxm);
@@ -1180,6 +1183,7 @@ GrB_Info GrB_Semiring_new(GrB_Semiring *semiring, GrB_Monoid add, GrB_BinaryOp m
 #define GB_DEFINE_TYPED_OPS(T, ctype)                                                                          \
     GrB_Info GrB_Vector_assign_##T(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum, ctype x,   \
                                    const GrB_Index *I, GrB_Index ni, const GrB_Descriptor desc) {            \
+        GB_HPROF(8, "GrB_Vector_assign scalar");                                                             \
         return gb_api(OBJ(w), [&] {                                                                          \
             vector_assign_scalar(gb_obj_check(w), gb_obj_check(mask, true), accum, &x, GBAMD_T_##T, I,       \
                                  (int64_t)ni, gb_read_desc(desc));                                           \
