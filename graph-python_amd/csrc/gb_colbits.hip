@@ -341,55 +341,6 @@ GB_DEV void cb_finish(const cb_step_args &a, long long cnt, long long hint) {
     }
 }
 
-// XCD-sliced pull: blocks b with b % 8 == c (dispatched to XCD c) walk only the
-// in-edges whose source lies in column slice c of the pull CSR (the cached slice-major
-// copy, gb_spmv_sliced.hip), so their F gathers stay inside one n/8-word range that
-// the XCD's L2 holds; each slice writes its partial words, k_cw_combine ORs them.
-__global__ __launch_bounds__(CB_BLOCK) void k_cw_pull_sl(cb_step_args a, const int32_t *__restrict__ srp,
-                                                          const int32_t *__restrict__ scol,
-                                                          const int64_t *__restrict__ sbase, uint64_t *part) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int c = blockIdx.x % 8;
-    const int64_t wave = (int64_t)(blockIdx.x / 8) * (CB_BLOCK / 64) + wid;
-    const int64_t nwaves = (int64_t)(gridDim.x / 8) * (CB_BLOCK / 64);
-    const bool m_on = !a.m_iso || gb_dyn_nonzero(a.m_iso, a.m_iso_code);
-    const bool use_sum = a.S_in && a.stat_in[2] == 1 && a.stat_in[0] * 4 < a.nin;
-    const int32_t *rp = srp + (int64_t)c * (a.nout + 1);
-    const int32_t *ci = scol + sbase[c];
-    uint64_t *pc = part + (int64_t)c * a.nout;
-    __shared__ uint64_t lacc[CB_BLOCK / 64][64];
-    uint64_t *acc_w = lacc[wid];
-    for (int64_t base = wave * 64; base < a.nout; base += nwaves * 64) {
-        const int64_t j = base + lane;
-        uint64_t need = 0;
-        bool hub = false;
-        cb_pull_chunk(a, j, m_on, use_sum, rp, ci, false, 0, acc_w, need, hub);
-        if (j < a.nout) pc[j] = acc_w[lane] & need;
-    }
-}
-
-// out[j] = OR of the 8 slices' partial words; count, edge hint, summary, publish
-__global__ __launch_bounds__(CB_BLOCK) void k_cw_combine(cb_step_args a, const uint64_t *__restrict__ part) {
-    const int lane = threadIdx.x & 63;
-    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    long long cnt = 0, hint = 0;
-    for (int64_t base = wave * 64; base < a.nout; base += nwaves * 64) {
-        const int64_t j = base + lane;
-        uint64_t w = 0;
-        if (j < a.nout) {
-#pragma unroll
-            for (int c = 0; c < 8; c++) w |= part[(int64_t)c * a.nout + j];
-            a.out[j] = w;
-            cnt += __popcll(w);
-            if (w && a.srp && j < a.nin) hint += a.srp[j + 1] - a.srp[j];
-        }
-        const uint64_t sb = __ballot(w != 0);
-        if (lane == 0) a.S_out[base >> 6] = sb;
-    }
-    cb_finish(a, cnt, hint);
-}
-
 // stat[1] = out-edges (rows of srp) of the non-empty columns of F
 __global__ __launch_bounds__(CB_BLOCK) void k_cw_hint(const uint64_t *__restrict__ F, int64_t n,
                                                        const int64_t *__restrict__ srp, int64_t *__restrict__ stat,
@@ -908,41 +859,11 @@ bool gb_colbits_mxm(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, GrB_Semiring sr, G
     a.s_tab = (dir != 1) ? sv.hubs : nullptr;
     a.s_nhub = (dir != 1 && sv.hubs) ? sv.nhubs : 0;
     a.H = H;
-    // host-side direction when the producer of A published its edge hint (the BFS loop
-    // has read A's count from the same mailbox): pull then runs XCD-sliced
-    bool sliced_pull = false;
-    // measured slower at R-MAT s22 (0.96-1.0 ms vs 0.85-0.90 ms per pull level): opt-in
-    int64_t sl_knob = gb_knob("colbits_sliced");  // 0 never, 1 always (pull), 3 when the host knows it pulls
-    sl_knob = sl_knob == 0 ? 2 : sl_knob == 3 ? 0 : sl_knob;
-    if (sl_knob != 2 && dir != 2 && bc >= 64 * 8 && (sl_knob == 1 || dir == 1)) {
-        sliced_pull = true;
-    } else if (sl_knob != 2 && dir != 2 && A->pub && A->pub_seq && A->hint_valid &&
-               A->hint_key == (const void *)sv.rowptr && bc >= 64 * 8) {
-        const long long seq_now = __atomic_load_n(&A->pub->seq, __ATOMIC_ACQUIRE);
-        if (seq_now == (long long)A->pub_seq) {
-            const long long h = __atomic_load_n(&A->pub->pad[0], __ATOMIC_RELAXED);
-            sliced_pull = dir == 1 || sl_knob == 1 || !(h * a.alpha < a.nnz);
-        }
-    }
-    if (sliced_pull) gb_view_slices(pv, B, d.tran1 ? 0 : 1);
-    if (sliced_pull && pv.sl_colidx) {
-        gb_scratch s;
-        uint64_t *part = s.get<uint64_t>((size_t)8 * bc);
-        unsigned g = cb_grid(bc, 2048);
-        g = (g + 7) / 8 * 8;
-        hipLaunchKernelGGL(k_cw_pull_sl, dim3(g), dim3(CB_BLOCK), 0, gb_stream(), a, pv.sl_rowptr, pv.sl_colidx,
-                           pv.sl_base, part);
-        GB_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_cw_combine, dim3(cb_grid(bc, 2048)), dim3(CB_BLOCK), 0, gb_stream(), a,
-                           (const uint64_t *)part);
-        GB_LAUNCH_CHECK();
-    } else {
-        // enough waves to cover the output in a few chunks each; every block joins the grid sums
-        const int64_t gcap = gb_knob("colbits_grid");
-        hipLaunchKernelGGL(k_cw_step, dim3(cb_grid((bc > inner ? bc : inner), gcap > 0 ? (unsigned)gcap : 2048)),
-                           dim3(CB_BLOCK), 0, gb_stream(), a);
-        GB_LAUNCH_CHECK();
-    }
+    // enough waves to cover the output in a few chunks each; every block joins the grid sums
+    const int64_t gcap = gb_knob("colbits_grid");
+    hipLaunchKernelGGL(k_cw_step, dim3(cb_grid((bc > inner ? bc : inner), gcap > 0 ? (unsigned)gcap : 2048)),
+                       dim3(CB_BLOCK), 0, gb_stream(), a);
+    GB_LAUNCH_CHECK();
 
     // install into C (stream-ordered frees: the kernel has read A/M before they go)
     if (C->kind == GB_KIND_MATRIX && !C->cw) {

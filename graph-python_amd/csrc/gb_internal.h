@@ -105,14 +105,6 @@ struct GB_Matrix_opaque {
     // cached long-row chunk tables (general SpMV, gb_mxv.hip)
     int32_t *long_tab[2];
     int64_t long_n[2];
-    // cached column-sliced copies (general SpMV with a dense input, gb_spmv_sliced.hip)
-    int32_t *sl_rowptr[2];
-    int32_t *sl_colidx[2];
-    void *sl_vals[2];
-    int64_t sl_base[2][9];
-    int64_t *sl_dbase[2];   // device [18]: slice entry bases [0..8], long-chunk table bases [9..17]
-    int32_t *sl_ltab[2];    // (row, chunk) pairs of the slices' long rows
-    int64_t sl_lcount[2];
     // ---- bitmap (kind == VECTOR / SCALAR); length n = nrows (ncols == 1)
     uint64_t *bits;      // [ceil(n/64)]
     void *dense;         // [n] or [1] when iso
@@ -305,14 +297,6 @@ struct gb_csr_view {
     int64_t maxdeg = -1;                 // longest row (host; attached with the hub chunks, -1 unknown)
     const int32_t *lchunks = nullptr;    // long-row chunks (row, piece) of the general SpMV (when attached)
     int64_t nlchunks = -1;
-    // column-sliced copy (when attached): 8 slice CSRs, int32 row pointers [8][nrows+1]
-    // relative to each slice's base, entries at sl_base[c] + ...
-    const int32_t *sl_rowptr = nullptr;
-    const int32_t *sl_colidx = nullptr;
-    const void *sl_vals = nullptr;
-    const int64_t *sl_base = nullptr;  // device [18] (entry bases, long-chunk table bases)
-    const int32_t *sl_ltab = nullptr;
-    int64_t sl_lcount = 0;
     gb_scratch own;
 };
 void gb_get_csr(gb_csr_view &v, GB_Obj *A);
@@ -325,8 +309,6 @@ void gb_view_nonempty(gb_csr_view &v, GB_Obj *A, int orient);
 // rows of at most 4 entries without reading their bounds or edges
 void gb_view_pullfirst(gb_csr_view &v, GB_Obj *A, int orient, const int64_t *other_rowptr, int64_t other_n);
 void gb_view_long_rows(gb_csr_view &v, GB_Obj *A, int orient);
-// attach (building on first use) the column-sliced copy of matrix A's orientation
-void gb_view_slices(gb_csr_view &v, GB_Obj *A, int orient);
 // CSC of A (i.e. CSR of A^T), cached on the object when A is a matrix.
 void gb_get_csc(gb_csr_view &v, GB_Obj *A);
 // the cached CSC of a matrix and, per CSC entry, its CSR position (built on first use)

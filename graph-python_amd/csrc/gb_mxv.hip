@@ -1459,10 +1459,6 @@ static int64_t iso_work_resident_blocks() {
     return cap;
 }  // keeps the prep/push/pull launches of one call adjacent
 
-// gb_spmv_sliced.hip: dense u, column-sliced by XCD
-bool gb_spmv_sliced(gb_vec_result &T, const gb_csr_view &A, const void *uv, bool u_iso, const gb_vmask &mask,
-                    GrB_Semiring sr, bool flip);
-
 bool gb_spmv_result_iso(GrB_Semiring sr, bool a_iso, bool u_iso, bool flip) {
     gb_sr_info info = gb_sr_describe(sr);
     bool reads_a = info.reads_values, reads_u = info.reads_values;
@@ -1494,8 +1490,6 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
         gb_memset(T.d_nvals, 0, sizeof(int64_t));
         return;
     }
-
-    if (!iso && u.full && A.sl_colidx && gb_spmv_sliced(T, A, uv, u.iso, mask, sr, flip)) return;
 
     const int64_t dir_knob = gb_knob("spmv_direction");  // 0 auto, 1 pull only, 2 push only
     const bool can_push = iso && Apush && Apush->nrows == u.n && Apush->hubs && dir_knob != 1;

@@ -136,17 +136,6 @@ void gb_drop_transpose(GB_Obj *A) {
         gb_free(A->long_tab[o]);
         A->long_tab[o] = nullptr;
         A->long_n[o] = 0;
-        gb_free(A->sl_rowptr[o]);
-        gb_free(A->sl_colidx[o]);
-        gb_free(A->sl_vals[o]);
-        gb_free(A->sl_dbase[o]);
-        gb_free(A->sl_ltab[o]);
-        A->sl_ltab[o] = nullptr;
-        A->sl_lcount[o] = 0;
-        A->sl_rowptr[o] = nullptr;
-        A->sl_colidx[o] = nullptr;
-        A->sl_vals[o] = nullptr;
-        A->sl_dbase[o] = nullptr;
     }
 }
 

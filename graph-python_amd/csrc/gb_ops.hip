@@ -81,12 +81,7 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
     const gb_csr_view *push = nullptr;
     const bool iso_result = gb_spmv_result_iso(sr, A->iso, uv.iso, vxm);
     if (!iso_result) gb_view_long_rows(av, A, use_csc ? 1 : 0);
-    // dense u, values out: the column-sliced kernel, opt-in (knob spmv_sliced = 2): it raises
-    // the L2 hit rate of the gathers (37 % -> 71-78 % at R-MAT s22) but its per-(row, slice)
-    // work costs more than it saves there (1.15 ms vs 0.92 ms)
     uv.full = u->kind != GB_KIND_MATRIX && u->nvals_valid && u->nvals == u->nrows && u->nrows > 0;
-    if (!iso_result && uv.full && A->kind == GB_KIND_MATRIX && gb_knob("spmv_sliced") == 2)
-        gb_view_slices(av, A, use_csc ? 1 : 0);
     if (A->kind == GB_KIND_MATRIX && gb_knob("spmv_direction") != 1 && iso_result) {
         if (use_csc) gb_get_csr(pv, A);
         else gb_get_csc(pv, A);

@@ -15,9 +15,14 @@ reduction into GraphBLAS calls:
   apply (:286-353).
 
 Row/column reductions thus run on the general SpMV kernel (gb_mxv.hip
-k_spmv_words) with no host round trip.  first/last/argmin/argmax (custom
-positional aggregators, :355-470) are not provided.
+k_spmv_words) with no host round trip.  The positional aggregators
+(``agg.ss.first/last/first_index/last_index/argmin/argmax``, reference :478-696)
+run on the positional semirings (min/max_secondi, min_firstj), any_eq mxm and
+a masked any_first mxm, as the reference lowers them; the diagonal matrices
+the reference takes with ``diag()`` are built from the step vector's COO.
 """
+from functools import partial
+
 import numpy as np
 
 from . import operator as _op
@@ -45,8 +50,9 @@ class Aggregator:
     opclass = "Aggregator"
 
     def __init__(self, name, *, initval=None, monoid=None, semiring=None, switch=False, semiring2=None,
-                 applybegin=None, finalize=None, composite=None, types=None, any_dtype=None):
+                 applybegin=None, finalize=None, composite=None, custom=None, types=None, any_dtype=None):
         self.name = name
+        self._custom = custom
         self._initval_orig = initval
         self._initval = False if initval is None else initval
         self._initdtype = lookup_dtype(np.asarray(self._initval).dtype)
@@ -89,7 +95,7 @@ class Aggregator:
         return self._any_dtype or dtype in self.types
 
     def __repr__(self):
-        return f"agg.{self.name}"
+        return f"agg.ss.{self.name}" if self._custom is not None else f"agg.{self.name}"
 
     def __call__(self, val, *, rowwise=False, columnwise=False):
         """agg(v) / agg(A, rowwise=True) sugar for the reduce methods (reference agg.py:111-138)."""
@@ -154,6 +160,8 @@ def _finalize(agg, v):
 
 def _rows(A, agg, dtype, opts):
     """Vector of per-row aggregates of A (A may be a TransposedMatrix)."""
+    if agg._custom is not None:
+        return agg._custom(agg, "rows", A, opts)
     if agg._monoid is not None:
         mon = _op.get_typed_op(agg._monoid, dtype, kind="monoid")
         return A.reduce_rowwise(mon).new(**opts)
@@ -177,6 +185,8 @@ def _to_scalar(w, agg, opts):
     """Scalar aggregate of a Vector (reference agg.py:229-248), as a 1-element Vector."""
     from .matrix import Matrix
 
+    if agg._custom is not None:
+        return agg._custom(agg, "vector", w, opts)
     if agg._monoid is not None:
         mon = _op.get_typed_op(agg._monoid, w.dtype, kind="monoid")
         from .vector import Vector
@@ -207,6 +217,8 @@ def _matrix_to_scalar(A, agg, opts):
     """Matrix -> Vector -> Scalar in two SpMVs (reference agg.py:249-276)."""
     from .vector import Vector
 
+    if agg._custom is not None:
+        return agg._custom(agg, "matrix", A, opts)
     if agg._monoid is not None:
         mon = _op.get_typed_op(agg._monoid, A.dtype, kind="monoid")
         out = Vector(mon.return_type, 1)
@@ -234,6 +246,117 @@ def _matrix_to_scalar(A, agg, opts):
     if agg._finalize is not None:
         step2 = _finalize(agg, step2)
     return step2
+
+
+# ---------------------------------------------------------------- positional aggregators
+def _false_vector(n):
+    from .dtypes import BOOL
+
+    return _iso_vector(BOOL, n, False)
+
+
+def _false_column(n):
+    """n x 1 iso-False matrix (the reference's "O(1) dense column vector", agg.py:520)."""
+    from .dtypes import BOOL
+    from .matrix import Matrix
+
+    m = Matrix(BOOL, n, 1, name="agg_init")
+    m[:, :] = False
+    return m
+
+
+def _one_vector(dtype, value):
+    from .vector import Vector
+
+    out = Vector(dtype, 1)
+    if value is not None:
+        out[0] = value
+    return out
+
+
+def _diag_of(w, n):
+    """diag(w) as an n x n Matrix (reference uses Vector.diag(), agg.py:494)."""
+    from .matrix import Matrix
+
+    idx, vals = w.to_coo()
+    return Matrix.from_coo(idx, idx, vals, dtype=w.dtype, nrows=n, ncols=n)
+
+
+def matrix_scalar_forbidden(agg):
+    """Name of the (sub-)aggregator of `agg` that has no Matrix.reduce_scalar form, or None
+    (reference agg.py:564-565, 664-665: argmin/argmax/first_index/last_index)."""
+    if getattr(agg, "_no_matrix_scalar", False):
+        return agg.name
+    for sub in agg._composite or ():
+        bad = matrix_scalar_forbidden(sub)
+        if bad:
+            return bad
+    return None
+
+
+def _argminmax(agg, kind, x, opts, *, monoid):
+    """argmin/argmax (reference agg.py:478-566): the row extremum, any_eq against it through a
+    diagonal, the true entries kept (value mask), then the least column index by min_firstj."""
+    from .dtypes import INT64
+
+    S = _op.semiring
+    if kind == "rows":
+        mon = _op.get_typed_op(monoid, x.dtype, kind="monoid")
+        step1 = x.reduce_rowwise(mon).new(**opts)
+        D = _diag_of(step1, x.nrows)
+        masked = D.mxm(x, S.any_eq).new(**opts)
+        masked(mask=masked.V, replace=True, **opts) << masked
+        return masked.mxv(_false_vector(x.ncols), S.min_firstj).new(**opts)
+    if kind == "vector":
+        mon = _op.get_typed_op(monoid, x.dtype, kind="monoid")
+        s = x.reduce(mon).new()
+        if s.value is None:
+            return _one_vector(INT64, None)
+        masked = x.apply(_op.binary.eq, right=s.value).new(**opts)
+        masked(mask=masked.V, replace=True, **opts) << masked
+        return masked.vxm(_false_column(x.size), S.min_secondi).new(**opts)
+    raise ValueError(f"Aggregator {agg.name} may not be used with Matrix.reduce_scalar.")
+
+
+def _first_last(agg, kind, x, opts, *, semiring_):
+    """first/last (reference agg.py:582-628): the position of each row's first (last) entry by
+    min_secondi (max_secondi), then its value through a masked any_first product with the
+    permutation-like matrix P[j_i, i] (the diagonal keeps only row i's pick)."""
+    from .dtypes import BOOL
+    from .matrix import Matrix
+
+    S = _op.semiring
+    if kind == "rows":
+        pos = x.mxv(_false_vector(x.ncols), semiring_).new(**opts)
+        I, J = pos.to_coo()
+        P = Matrix.from_coo(J, I, True, dtype=BOOL, nrows=x.ncols, ncols=x.nrows)
+        D = Matrix.from_coo(I, I, True, dtype=BOOL, nrows=x.nrows, ncols=x.nrows)
+        C = Matrix(x.dtype, x.nrows, x.nrows, name="agg_pick")
+        C(mask=D.S, **opts) << x.mxm(P, S.any_first)
+        return C.reduce_rowwise(_op.monoid.any).new(**opts)
+    if kind == "vector":
+        pos = x.vxm(_false_column(x.size), semiring_).new(**opts)
+        i = pos[0].value if pos.nvals else None
+        return _one_vector(x.dtype, None if i is None else x[int(i)].value)
+    # Matrix.reduce_scalar: the first (last) row holding entries, then its first (last) column
+    step1 = x.mxm(_false_column(x.ncols), semiring_).new(**opts)
+    step2 = step1.T.mxv(_false_vector(x.nrows), semiring_).new(**opts)
+    i = step2[0].value if step2.nvals else None
+    if i is None:
+        return _one_vector(x.dtype, None)
+    j = step1[int(i), 0].value
+    M, (r, c) = (x._matrix, (int(j), int(i))) if hasattr(x, "_matrix") else (x, (int(i), int(j)))
+    return _one_vector(x.dtype, M[r, c].value)
+
+
+def _first_last_index(agg, kind, x, opts, *, semiring_):
+    """first_index/last_index (reference agg.py:645-667): min_secondi / max_secondi against an
+    iso-False vector gives each row's first / last column index directly."""
+    if kind == "rows":
+        return x.mxv(_false_vector(x.ncols), semiring_).new(**opts)
+    if kind == "vector":
+        return x.vxm(_false_column(x.size), semiring_).new(**opts)
+    raise ValueError(f"Aggregator {agg.name} may not be used with Matrix.reduce_scalar.")
 
 
 def reduce_rowwise_recipe(updater, A, typed, columnwise):
@@ -377,5 +500,32 @@ agg.harmonic_mean = Aggregator("harmonic_mean", composite=[agg.count, agg.sum_of
                                finalize=_harmonic_mean, types=[_truediv_types])
 agg.root_mean_square = Aggregator("root_mean_square", composite=[agg.count, agg.sum_of_squares],
                                   finalize=_root_mean_square, types=[_truediv_types])
+
+# positional aggregators (reference agg.py:569-696; SuiteSparse-only there, so under agg.ss)
+_sr = _op.semiring
+_argmin = Aggregator("argmin", custom=partial(_argminmax, monoid=_m.min), types=[_sr.min_firsti])
+_argmax = Aggregator("argmax", custom=partial(_argminmax, monoid=_m.max), types=[_sr.min_firsti])
+_first = Aggregator("first", custom=partial(_first_last, semiring_=_sr.min_secondi), types=[_op.binary.first],
+                    any_dtype=True)
+_last = Aggregator("last", custom=partial(_first_last, semiring_=_sr.max_secondi), types=[_op.binary.second],
+                   any_dtype=True)
+_first_index = Aggregator("first_index", custom=partial(_first_last_index, semiring_=_sr.min_secondi),
+                          types=[_sr.min_secondi], any_dtype=INT64)
+_last_index = Aggregator("last_index", custom=partial(_first_last_index, semiring_=_sr.max_secondi),
+                         types=[_sr.min_secondi], any_dtype=INT64)
+for _a in (_argmin, _argmax, _first_index, _last_index):
+    _a._no_matrix_scalar = True
+
+
+class _AggSS:
+    def __repr__(self):
+        return "agg.ss"
+
+
+agg.ss = _AggSS()
+for _a in (_argmin, _argmax, _first, _last, _first_index, _last_index):
+    setattr(agg.ss, _a.name, _a)
+agg._deprecated = {a.name: a for a in (_argmin, _argmax, _first, _last, _first_index, _last_index)}
+
 agg.Aggregator = Aggregator
 agg.TypedAggregator = TypedAggregator

@@ -589,9 +589,12 @@ def _reduce_scalar(x, op, allow_empty):
     if op is None:
         op = _op.monoid.plus
     if _is_agg(op):
-        from .agg import reduce_scalar_recipe
+        from .agg import matrix_scalar_forbidden, reduce_scalar_recipe
 
         typed = op[x.dtype] if not hasattr(op, "parent") else op
+        bad = matrix_scalar_forbidden(typed.parent) if x.ndim == 2 else None
+        if bad:
+            raise ValueError(f"Aggregator {bad} may not be used with Matrix.reduce_scalar.")
         if not allow_empty:
             if typed.parent._monoid is None:
                 raise ValueError("allow_empty=False not allowed when using Aggregators")

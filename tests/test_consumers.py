@@ -327,3 +327,118 @@ def test_scan_matrix_random_vs_numpy(gb):
         assert np.array_equal(r.astype(np.int64), rows) and np.array_equal(c.astype(np.int64), cols)
         exp = np.concatenate([fn(vals[starts[i]:starts[i + 1]]) for i in range(n) if deg[i]])
         assert np.array_equal(rv, exp)
+
+
+# ------------------------------------------------------------------ positional aggregators
+# Expected values: reference graphblas/tests/test_matrix.py test_reduce_agg_argminmax :1458,
+# test_reduce_agg_firstlast :1510, test_reduce_agg_firstlast_index :1566;
+# graphblas/tests/test_vector.py :952-997.
+def test_reduce_agg_argminmax_matrix(gb, A):
+    agg = gb.agg
+    for op, exp in [(agg.ss.argmin, [1, 6, 5, 0, 5, 2, 4]), (agg.ss.argmax, [3, 4, 5, 0, 5, 2, 3])]:
+        assert A.reduce_rowwise(op).new().isequal(V(gb, range(7), exp))
+        assert A.T.reduce_columnwise(op).new().isequal(V(gb, range(7), exp))
+    for op, exp in [(agg.ss.argmin, [3, 0, 5, 0, 6, 2, 1]), (agg.ss.argmax, [3, 0, 6, 6, 1, 4, 1])]:
+        assert A.reduce_columnwise(op).new().isequal(V(gb, range(7), exp))
+        assert A.T.reduce_rowwise(op).new().isequal(V(gb, range(7), exp))
+    with pytest.raises(ValueError, match="Aggregator argmin may not be used with Matrix.reduce_scalar"):
+        A.reduce_scalar(agg.ss.argmin)
+    silly = agg.Aggregator("silly", composite=[agg.ss.argmin, agg.ss.argmax],
+                           finalize=lambda x, y, opts: gb.binary.plus(x & y), types=[agg.ss.argmin])
+    for method in ("reduce_rowwise", "reduce_columnwise"):
+        v1 = getattr(A, method)(agg.ss.argmin).new()
+        v2 = getattr(A, method)(agg.ss.argmax).new()
+        v3 = getattr(A, method)(silly).new()
+        assert v3.isequal(gb.binary.plus(v1 & v2).new())
+    with pytest.raises(ValueError, match="Aggregator"):
+        A.reduce_scalar(silly).new()
+
+
+def test_reduce_agg_firstlast_matrix(gb, A):
+    agg = gb.agg
+    cases = [("reduce_rowwise", agg.ss.first, [2, 8, 1, 3, 7, 1, 5]),
+             ("reduce_rowwise", agg.ss.last, [3, 4, 1, 3, 7, 1, 3]),
+             ("reduce_columnwise", agg.ss.first, [3, 2, 3, 3, 8, 1, 4]),
+             ("reduce_columnwise", agg.ss.last, [3, 2, 5, 7, 3, 7, 4])]
+    other = {"reduce_rowwise": "reduce_columnwise", "reduce_columnwise": "reduce_rowwise"}
+    for method, op, exp in cases:
+        assert getattr(A, method)(op).new().isequal(V(gb, range(7), exp))
+        assert getattr(A.T, other[method])(op).new().isequal(V(gb, range(7), exp))
+    assert A.reduce_scalar(agg.ss.first).new() == 2
+    assert A.reduce_scalar(agg.ss.last).new() == 3
+    B = gb.Matrix(float, nrows=2, ncols=3)
+    assert B.reduce_scalar(agg.ss.first).new().is_empty
+    assert B.reduce_scalar(agg.ss.last).new().is_empty
+    assert B.reduce_rowwise(agg.ss.first).new().isequal(gb.Vector(float, size=B.nrows))
+    assert B.reduce_columnwise(agg.ss.last).new().isequal(gb.Vector(float, size=B.ncols))
+    silly = agg.Aggregator("silly", composite=[agg.ss.first, agg.ss.last],
+                           finalize=lambda x, y, opts: gb.binary.plus(x & y), types=[agg.ss.first])
+    v1 = A.reduce_rowwise(agg.ss.first).new()
+    v2 = A.reduce_rowwise(agg.ss.last).new()
+    assert A.reduce_rowwise(silly).new().isequal(gb.binary.plus(v1 & v2).new())
+    s1 = A.reduce_scalar(agg.ss.first).new()
+    s2 = A.reduce_scalar(agg.ss.last).new()
+    assert A.reduce_scalar(silly).new().isequal(s1.value + s2.value)
+
+
+def test_reduce_agg_firstlast_index_matrix(gb, A):
+    agg = gb.agg
+    cases = [("reduce_rowwise", agg.ss.first_index, [1, 4, 5, 0, 5, 2, 2]),
+             ("reduce_rowwise", agg.ss.last_index, [3, 6, 5, 2, 5, 2, 4]),
+             ("reduce_columnwise", agg.ss.first_index, [3, 0, 3, 0, 1, 2, 1]),
+             ("reduce_columnwise", agg.ss.last_index, [3, 0, 6, 6, 6, 4, 1])]
+    other = {"reduce_rowwise": "reduce_columnwise", "reduce_columnwise": "reduce_rowwise"}
+    for method, op, exp in cases:
+        assert getattr(A, method)(op).new().isequal(V(gb, range(7), exp))
+        assert getattr(A.T, other[method])(op).new().isequal(V(gb, range(7), exp))
+    with pytest.raises(ValueError, match="Aggregator first_index may not"):
+        A.reduce_scalar(agg.ss.first_index).new()
+    with pytest.raises(ValueError, match="Aggregator last_index may not"):
+        A.reduce_scalar(agg.ss.last_index).new()
+    silly = agg.Aggregator("silly", composite=[agg.ss.first_index, agg.ss.last_index],
+                           finalize=lambda x, y, opts: gb.binary.plus(x & y), types=[agg.ss.first_index])
+    v1 = A.reduce_rowwise(agg.ss.first_index).new()
+    v2 = A.reduce_rowwise(agg.ss.last_index).new()
+    assert A.reduce_rowwise(silly).new().isequal(gb.binary.plus(v1 & v2).new())
+    with pytest.raises(ValueError, match="Aggregator"):
+        A.reduce_scalar(silly).new()
+
+
+def test_reduce_agg_positional_vector(gb, v):
+    agg = gb.agg
+    assert v.reduce(agg.ss.argmin).new() == 6
+    assert v.reduce(agg.ss.argmax).new() == 4
+    empty = gb.Vector(int, size=4)
+    assert empty.reduce(agg.ss.first).new().is_empty
+    assert empty.reduce(agg.ss.last).new().is_empty
+    assert v.reduce(agg.ss.first).new() == 1
+    assert v.reduce(agg.ss.last).new() == 0
+    assert v.reduce(agg.ss.first_index).new() == 1
+    assert v.reduce(agg.ss.last_index).new() == 6
+    for parts, expect in [((agg.ss.argmin, agg.ss.argmax), 10), ((agg.ss.first, agg.ss.last), 1),
+                          ((agg.ss.first_index, agg.ss.last_index), 7)]:
+        silly = agg.Aggregator("silly", composite=list(parts),
+                               finalize=lambda x, y, opts: gb.binary.plus(x & y), types=[parts[0]])
+        assert v.reduce(silly).new() == expect
+    assert repr(agg.ss.first) == "agg.ss.first"
+
+
+def test_reduce_agg_positional_random_vs_numpy(gb):
+    """Seeded 40 x 50 int64 matrix: row argmin/argmax/first/last vs numpy on the same entries."""
+    rng = np.random.default_rng(11)
+    dense = rng.integers(-5, 6, size=(40, 50))
+    keep = rng.random((40, 50)) < 0.2
+    r, c = np.nonzero(keep)
+    M = gb.Matrix.from_coo(r, c, dense[r, c], nrows=40, ncols=50)
+    got = {k: dict(zip(*getattr(M.reduce_rowwise(getattr(gb.agg.ss, k)).new(), "to_coo")()))
+           for k in ("argmin", "argmax", "first", "last", "first_index", "last_index")}
+    for i in range(40):
+        cols = np.nonzero(keep[i])[0]
+        if cols.size == 0:
+            assert all(i not in g for g in got.values())
+            continue
+        vals = dense[i, cols]
+        assert got["argmin"][i] == cols[np.argmin(vals)]
+        assert got["argmax"][i] == cols[np.argmax(vals)]
+        assert got["first"][i] == vals[0] and got["last"][i] == vals[-1]
+        assert got["first_index"][i] == cols[0] and got["last_index"][i] == cols[-1]

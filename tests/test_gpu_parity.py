@@ -882,70 +882,3 @@ def test_masked_spgemm_two_sided_vs_oracle(gb, name, mon, mul, dt, knobs, form):
         assert np.array_equal(r.astype(np.int64), er) and np.array_equal(c.astype(np.int64), ec)
     else:
         _check_mat(Cg, ref)
-
-
-SLICED = [
-    ("plus_times", "PLUS", "TIMES", "FP64"),
-    ("plus_times", "PLUS", "TIMES", "FP32"),
-    ("min_plus", "MIN", "PLUS", "INT64"),
-    ("max_times", "MAX", "TIMES", "INT32"),
-    ("plus_pair", "PLUS", "PAIR", "INT64"),
-    ("min_first", "MIN", "FIRST", "UINT64"),
-    ("plus_secondi", "PLUS", "SECONDI", "INT64"),
-]
-
-
-@pytest.mark.parametrize("name,mon,mul,dt", SLICED)
-@pytest.mark.parametrize("kind", ["vxm", "mxv_T", "mxv_mask", "vxm_comp_mask", "iso_A"])
-def test_sliced_spmv_vs_oracle(gb, name, mon, mul, dt, kind):
-    """The column-sliced SpMV (gb_spmv_sliced.hip; knob spmv_sliced 2 forces it at any
-    size): dense u, eight slice CSRs folded in slice order, mask applied in the combine.
-    Rows of very different lengths (empty, short, > 128, a full row).  Bit-exact for
-    exact monoids, rtol 1e-12 (fp64) / 1e-5 (fp32) for plus."""
-    rng = np.random.default_rng(zlib.crc32(repr((name, dt, kind, "sliced")).encode()))
-    n = 1500
-    Ao = _skewed_csr(rng, n, dt)
-    if kind == "iso_A":
-        r, c, _ = Ao.to_coo()
-        Ao = O.Csr.from_coo(r, c, np.full(r.size, 3, O.NP[dt]), nrows=n, ncols=n, dtype=dt)
-        Ag = gb.Matrix.from_coo(r, c, 3, dtype=dt, nrows=n, ncols=n)
-    else:
-        Ag = _to_gb(gb, Ao)
-    if dt in ("FP32", "FP64"):
-        uvals = rng.standard_normal(n).astype(O.NP[dt])
-    else:
-        uvals = rng.integers(-30, 30, n).astype(O.NP[dt])
-    u = O.Vec(n, dt, np.arange(n), uvals)
-    ug = gb.Vector.from_coo(np.arange(n), uvals, dtype=dt, size=n)
-    mo = _rand_csr(rng, n, 1, 0.5, "BOOL")
-    m = O.Vec.from_col(mo)
-    mg = gb.Vector.from_coo(m.indices, m.values, dtype="BOOL", size=n)
-    sr = getattr(gb.semiring, name)[dt]
-    w0 = O.Vec(n, dt, np.zeros(0, np.int64), np.zeros(0, O.NP[dt]))
-    wg = gb.Vector(dt, n)
-    gb.set_knob("spmv_sliced", 2)
-    try:
-        if kind in ("vxm", "iso_A"):
-            wg << ug.vxm(Ag, sr)
-            ref = O.vxm(w0, u, Ao, (mon, mul, dt))
-        elif kind == "mxv_T":
-            wg << Ag.T.mxv(ug, sr)
-            ref = O.mxv(w0, Ao, u, (mon, mul, dt), tran0=True)
-        elif kind == "mxv_mask":
-            wg(mg.V) << Ag.mxv(ug, sr)
-            ref = O.mxv(w0, Ao, u, (mon, mul, dt), mask=m)
-        else:
-            wg(~mg.S, replace=True) << ug.vxm(Ag, sr)
-            ref = O.vxm(w0, u, Ao, (mon, mul, dt), mask=m, mask_comp=True, mask_struct=True, replace=True)
-    finally:
-        gb.set_knob("spmv_sliced", 0)
-    gi, gv = wg.to_coo()
-    assert np.array_equal(gi.astype(np.int64), ref.indices)
-    if dt in ("FP32", "FP64") and mon == "PLUS":
-        # slices fold in a different association than the oracle's ascending k: rows of up to
-        # 1500 terms ~N(0,1) cancel to small sums, so the bound is absolute (a few ulps of the
-        # terms' scale) as well as relative
-        np.testing.assert_allclose(gv, ref.values, rtol=1e-5 if dt == "FP32" else 1e-12,
-                                   atol=1e-4 if dt == "FP32" else 1e-9)
-    else:
-        assert np.array_equal(gv, ref.values)
