@@ -99,7 +99,22 @@ struct cb_step_args {
     uint64_t *S_out;                        // out's summary (zeroed)
     const int32_t *p_tab, *s_tab;           // hub pieces (row, piece) of the pull / push orientation
     int64_t p_nhub, s_nhub, H;
+    const uint64_t *Fhot;                   // pci relabelled (gb_view_hot): F of the hot sources, rank order
 };
+
+// the level pushes (same rule as k_cw_step)
+GB_DEV bool cb_pushes(const cb_step_args &a) {
+    return a.srp && (a.dir == 2 || (a.dir == 0 && a.stat_in[1] * a.alpha < a.nnz));
+}
+
+// F word of in-edge source i of the pull list: i < 0 names a hot source (relabelled pci),
+// whose word was packed into Fhot before the step; a sparse frontier tests the summary bit
+// (L2-resident) before gathering a cold word
+GB_DEV uint64_t cb_gather(const cb_step_args &a, int64_t i, bool use_sum) {
+    if (i < 0) return a.Fhot[i & 0x7fffffffLL];
+    if (use_sum && !((a.S_in[i >> 6] >> (i & 63)) & 1ULL)) return 0ULL;
+    return a.F[i];
+}
 
 GB_DEV uint64_t cb_need(const cb_step_args &a, int64_t j, bool m_on) {
     if (!a.M) return a.full;
@@ -129,10 +144,6 @@ GB_DEV void cb_pull_chunk(const cb_step_args &a, int64_t j, bool m_on, bool use_
                           const int32_t *__restrict__ ci, bool hubs, int64_t H, uint64_t *acc_w, uint64_t &need,
                           bool &hub) {
     const int lane = threadIdx.x & 63;
-    auto gather = [&](int64_t i) -> uint64_t {
-        if (use_sum && !((a.S_in[i >> 6] >> (i & 63)) & 1ULL)) return 0ULL;
-        return a.F[i];
-    };
     int64_t s0 = 0;
     int len = 0;
     if (j < a.nout) {
@@ -175,11 +186,11 @@ GB_DEV void cb_pull_chunk(const cb_step_args &a, int64_t j, bool m_on, bool use_
         for (int u = 0; u < CB_U; u++) {
             const int t = tb + 64 * u + lane;
             const int64_t q = (int64_t)t + cb_shfl_i64(eb, c[u] < 64 ? c[u] : 0);
-            src[u] = t < T ? ci[q] : -1;
+            src[u] = t < T ? ci[q] : 0;
         }
 #pragma unroll
         for (int u = 0; u < CB_U; u++)
-            if (src[u] >= 0) f[u] = gather(src[u]);
+            if (c[u] < 64) f[u] = cb_gather(a, src[u], use_sum);
 #pragma unroll
         for (int u = 0; u < CB_U; u++) {
             uint64_t x = f[u];
@@ -208,7 +219,7 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cw_step(cb_step_args a) {
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const bool m_on = !a.m_iso || gb_dyn_nonzero(a.m_iso, a.m_iso_code);
-    const bool push = a.srp && (a.dir == 2 || (a.dir == 0 && a.stat_in[1] * a.alpha < a.nnz));
+    const bool push = cb_pushes(a);
     // sparse frontier: test the summary bit (L2-resident) before gathering a word
     const bool use_sum = a.S_in && a.stat_in[2] == 1 && a.stat_in[0] * 4 < a.nin;
     const int64_t H = a.H;
@@ -224,10 +235,6 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cw_step(cb_step_args a) {
             if (a.srp && j < a.nin) hint += a.srp[j + 1] - a.srp[j];
         }
     };
-    auto gather = [&](int64_t i) -> uint64_t {
-        if (use_sum && !((a.S_in[i >> 6] >> (i & 63)) & 1ULL)) return 0ULL;
-        return a.F[i];
-    };
     if (!push) {
         // hub pieces: rows of the pull orientation longer than H
         for (int64_t t = wave; t < a.p_nhub; t += nwaves) {
@@ -242,7 +249,7 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cw_step(cb_step_args a) {
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
                     const int64_t q = qb + lane + 64 * u;
-                    if (q < end) f |= gather(a.pci[q]);
+                    if (q < end) f |= cb_gather(a, a.pci[q], use_sum);
                 }
                 acc |= cb_wave_or(f);
                 if ((acc & need) == need) break;
@@ -308,6 +315,14 @@ __global__ __launch_bounds__(CB_BLOCK) void k_cw_step(cb_step_args a) {
         }
     }
     cb_finish(a, cnt, hint);
+}
+
+// the hot sources' frontier words, packed in rank order for a pulling step (no-op when it pushes)
+__global__ __launch_bounds__(CB_BLOCK) void k_cw_hot_gather(cb_step_args a, const int32_t *__restrict__ hot,
+                                                             int64_t nh, uint64_t *__restrict__ Fhot) {
+    if (cb_pushes(a)) return;
+    for (int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; h < nh; h += (int64_t)gridDim.x * blockDim.x)
+        Fhot[h] = a.F[hot[h]];
 }
 
 // count and edge-hint grid sums; whichever block finishes the second one publishes
@@ -859,11 +874,26 @@ bool gb_colbits_mxm(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, GrB_Semiring sr, G
     a.s_tab = (dir != 1) ? sv.hubs : nullptr;
     a.s_nhub = (dir != 1 && sv.hubs) ? sv.nhubs : 0;
     a.H = H;
+    // pulls on a large graph read the in-edge sources' words through the hot-column relabel
+    // (gb_view_hot): the most frequent sources' words are packed first, L2-resident
+    uint64_t *Fhot = nullptr;
+    if (dir != 2 && gb_knob("colbits_hot") != 1) {
+        gb_view_hot(pv, B, d.tran1 ? 0 : 1);
+        if (pv.hcolidx) {
+            Fhot = gb_malloc_n<uint64_t>(pv.nhot);
+            hipLaunchKernelGGL(k_cw_hot_gather, dim3(cb_grid(pv.nhot, 1024)), dim3(CB_BLOCK), 0, gb_stream(), a,
+                               pv.hcols, pv.nhot, Fhot);
+            GB_LAUNCH_CHECK();
+            a.pci = pv.hcolidx;
+            a.Fhot = Fhot;
+        }
+    }
     // enough waves to cover the output in a few chunks each; every block joins the grid sums
     const int64_t gcap = gb_knob("colbits_grid");
     hipLaunchKernelGGL(k_cw_step, dim3(cb_grid((bc > inner ? bc : inner), gcap > 0 ? (unsigned)gcap : 2048)),
                        dim3(CB_BLOCK), 0, gb_stream(), a);
     GB_LAUNCH_CHECK();
+    gb_free(Fhot);  // stream-ordered
 
     // install into C (stream-ordered frees: the kernel has read A/M before they go)
     if (C->kind == GB_KIND_MATRIX && !C->cw) {

@@ -105,6 +105,12 @@ struct GB_Matrix_opaque {
     // cached long-row chunk tables (general SpMV, gb_mxv.hip)
     int32_t *long_tab[2];
     int64_t long_n[2];
+    // cached hot-column relabel (general SpMV with a dense input, gb_prim.hip gb_view_hot):
+    // colidx with the hot_n most frequent columns replaced by INT32_MIN | rank (rank in
+    // descending frequency), and the hot columns' original ids in rank order
+    int32_t *hot_ci[2];
+    int32_t *hot_cols[2];
+    int64_t hot_n[2];
     // ---- bitmap (kind == VECTOR / SCALAR); length n = nrows (ncols == 1)
     uint64_t *bits;      // [ceil(n/64)]
     void *dense;         // [n] or [1] when iso
@@ -297,6 +303,9 @@ struct gb_csr_view {
     int64_t maxdeg = -1;                 // longest row (host; attached with the hub chunks, -1 unknown)
     const int32_t *lchunks = nullptr;    // long-row chunks (row, piece) of the general SpMV (when attached)
     int64_t nlchunks = -1;
+    const int32_t *hcolidx = nullptr;    // hot-column relabelled colidx (when attached; see GB_Obj::hot_ci)
+    const int32_t *hcols = nullptr;      // the hot columns' original ids, rank order
+    int64_t nhot = 0;
     gb_scratch own;
 };
 void gb_get_csr(gb_csr_view &v, GB_Obj *A);
@@ -309,6 +318,9 @@ void gb_view_nonempty(gb_csr_view &v, GB_Obj *A, int orient);
 // rows of at most 4 entries without reading their bounds or edges
 void gb_view_pullfirst(gb_csr_view &v, GB_Obj *A, int orient, const int64_t *other_rowptr, int64_t other_n);
 void gb_view_long_rows(gb_csr_view &v, GB_Obj *A, int orient);
+// attach (building on first use) the hot-column relabel of matrix A's orientation, when the
+// matrix is large enough for the x gathers of a dense-input SpMV to miss in L2
+void gb_view_hot(gb_csr_view &v, GB_Obj *A, int orient);
 // CSC of A (i.e. CSR of A^T), cached on the object when A is a matrix.
 void gb_get_csc(gb_csr_view &v, GB_Obj *A);
 // the cached CSC of a matrix and, per CSC entry, its CSR position (built on first use)

@@ -720,11 +720,12 @@ struct gb_iso_args {
 template <class SR, class X, class Z, bool FLIP>
 __device__ __forceinline__ void gb_spmv_product(SR &sr, bool rv, const X *__restrict__ avals, bool a_iso, X a0,
                                                 const X *__restrict__ uvals, bool u_iso, X u0, int64_t p, int k,
-                                                int64_t r, Z &z) {
+                                                int64_t r, Z &z, const X *__restrict__ uhot) {
     X a = X(), b = X();
     if (rv) {
         a = a_iso ? a0 : avals[p];
-        b = u_iso ? u0 : uvals[k];
+        // k < 0: a hot column (relabelled colidx, gb_view_hot): its value from the packed copy
+        b = u_iso ? u0 : (k < 0 ? uhot[k & 0x7fffffff] : uvals[k]);
     }
     z = FLIP ? sr.mult(b, a, 0, k, r) : sr.mult(a, b, r, k, 0);
 }
@@ -747,7 +748,8 @@ __device__ __forceinline__ long long gb_spmv_words_mp(
     SR &sr, int64_t nrows, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ colidx,
     const X *__restrict__ avals, bool a_iso, X a0, const uint64_t *__restrict__ ubits, const X *__restrict__ uvals,
     bool u_iso, X u0, const uint64_t *__restrict__ mbits, bool mcomp, bool ufull, bool rv,
-    uint64_t *__restrict__ tbits, Z *__restrict__ tvals, Z *acc, int *fl, gb_mp_lds<Z> &M) {
+    uint64_t *__restrict__ tbits, Z *__restrict__ tvals, Z *acc, int *fl, gb_mp_lds<Z> &M,
+    const X *__restrict__ uhot) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -822,7 +824,7 @@ __device__ __forceinline__ long long gb_spmv_words_mp(
                         zt[t] = Z();
                         if (hit[t])
                             gb_spmv_product<SR, X, Z, FLIP>(sr, rv, avals, a_iso, a0, uvals, u_iso, u0, pos[t], k[t],
-                                                            (w << 6) + rw[t], zt[t]);
+                                                            (w << 6) + rw[t], zt[t], uhot);
                     }
 #pragma unroll
                     for (int t = 0; t < 4; t++) {
@@ -903,7 +905,8 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
     const X *__restrict__ uvals, bool u_iso, const uint64_t *__restrict__ mbits, bool mcomp,
     const int32_t *__restrict__ chunks, int64_t nchunks, Z *__restrict__ cpart, int8_t *__restrict__ cfound,
     uint64_t *__restrict__ tbits, Z *__restrict__ tvals, unsigned long long *__restrict__ tcount,
-    unsigned long long *__restrict__ gst, const int64_t *__restrict__ ucount, int64_t un, int mode) {
+    unsigned long long *__restrict__ gst, const int64_t *__restrict__ ucount, int64_t un, int mode,
+    const X *__restrict__ uhot) {
     __shared__ Z accs[WAVES_PER_BLOCK][64];
     __shared__ int fls[WAVES_PER_BLOCK][64];
     __shared__ gb_mp_lds<Z> mps[WAVES_PER_BLOCK];
@@ -919,7 +922,8 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
         if (a_iso) a0 = avals[0];
         if (u_iso) u0 = uvals[0];
     }
-    const bool ufull = ucount && *ucount == un;  // u has every entry: no presence tests
+    // u has every entry: no presence tests (a relabelled colidx, uhot, is used only then)
+    const bool ufull = uhot || (ucount && *ucount == un);
     fl[lane] = 0;
     gb_wave_sync();
     long long cnt = 0;
@@ -945,7 +949,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
                     if (!ok[u] || (!ufull && !gb_bit(ubits, kk[u]))) continue;
                     Z t;
                     gb_spmv_product<SR, X, Z, FLIP>(sr, rv, avals, a_iso, a0, uvals, u_iso, u0, q + 64 * u, kk[u],
-                                                    r, t);
+                                                    r, t, uhot);
                     z = f ? sr.add(z, t) : t;
                     f = true;
                 }
@@ -967,7 +971,8 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
     // output words
     if (mode == 1) {
         cnt += gb_spmv_words_mp<SR, X, Z, FLIP>(sr, nrows, rowptr, colidx, avals, a_iso, a0, ubits, uvals, u_iso, u0,
-                                                mbits, mcomp, ufull, rv, tbits, tvals, acc, fl, mps[threadIdx.x >> 6]);
+                                                mbits, mcomp, ufull, rv, tbits, tvals, acc, fl, mps[threadIdx.x >> 6],
+                                                uhot);
         long long tot;
         if (gb_grid_sum(cnt, gst, &tot)) *tcount = (unsigned long long)tot;
         return;
@@ -1015,7 +1020,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
                 zu[u] = Z();
                 if (fu[u])
                     gb_spmv_product<SR, X, Z, FLIP>(sr, rv, avals, a_iso, a0, uvals, u_iso, u0, pos[u], k[u],
-                                                    (w << 6) + own[u], zu[u]);
+                                                    (w << 6) + own[u], zu[u], uhot);
             }
 #pragma unroll
             for (int u = 0; u < SPMV_WU; u++) {
@@ -1054,6 +1059,14 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
     }
     long long tot;
     if (gb_grid_sum(cnt, gst, &tot)) *tcount = (unsigned long long)tot;  // k_spmv_fold adds the long rows
+}
+
+// the hot columns' values of a dense u, packed in rank order (gb_view_hot)
+template <class X>
+__global__ void k_hot_gather(const X *__restrict__ uvals, const int32_t *__restrict__ hcols, int64_t nh,
+                             X *__restrict__ uhot) {
+    for (int64_t h = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; h < nh; h += (int64_t)gridDim.x * blockDim.x)
+        uhot[h] = uvals[hcols[h]];
 }
 
 // long rows: fold their chunks' partials in chunk order (one thread per row)
@@ -1653,16 +1666,28 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             const bool u_iso_k = u.iso || gb_knob("spmv_timing_no_x_gather") == 1;  // timing experiment only
             const int spmv_mode = gb_knob("spmv_words") == 2 ? 1 : 0;  // 0: segmented scan (default), 2: merge path
             const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 3) / 4, 4096));
+            // dense u on a relabelled matrix: the hot columns' values packed first (gb_view_hot);
+            // positional multipliers need the true column, so they keep the plain colidx
+            const int32_t *ci = A.colidx;
+            X *uhot = nullptr;
+            if (A.hcolidx && u.full && !u_iso_k && uv && !info.positional && info.reads_values) {
+                uhot = s.get<X>(A.nhot);
+                const unsigned hg = (unsigned)std::max<int64_t>(1, std::min<int64_t>((A.nhot + 255) / 256, 2048));
+                hipLaunchKernelGGL((k_hot_gather<X>), dim3(hg), dim3(256), 0, gb_stream(), (const X *)uv, A.hcols,
+                                   A.nhot, uhot);
+                GB_LAUNCH_CHECK();
+                ci = A.hcolidx;
+            }
             if (flip)
                 hipLaunchKernelGGL((k_spmv_words<SRT, X, Z, true>), dim3(grid), dim3(SPMV_BLOCK), 0, gb_stream(), srf,
-                                   n, A.rowptr, A.colidx, (const X *)av, A.iso, u.bits, (const X *)uv, u_iso_k,
+                                   n, A.rowptr, ci, (const X *)av, A.iso, u.bits, (const X *)uv, u_iso_k,
                                    mask.bits, mask.comp, A.lchunks, A.nlchunks, cpart, cfound, T.bits, (Z *)T.dense,
-                                   (unsigned long long *)T.d_nvals, gst, u.count, u.n, spmv_mode);
+                                   (unsigned long long *)T.d_nvals, gst, u.count, u.n, spmv_mode, (const X *)uhot);
             else
                 hipLaunchKernelGGL((k_spmv_words<SRT, X, Z, false>), dim3(grid), dim3(SPMV_BLOCK), 0, gb_stream(),
-                                   srf, n, A.rowptr, A.colidx, (const X *)av, A.iso, u.bits, (const X *)uv, u_iso_k,
+                                   srf, n, A.rowptr, ci, (const X *)av, A.iso, u.bits, (const X *)uv, u_iso_k,
                                    mask.bits, mask.comp, A.lchunks, A.nlchunks, cpart, cfound, T.bits, (Z *)T.dense,
-                                   (unsigned long long *)T.d_nvals, gst, u.count, u.n, spmv_mode);
+                                   (unsigned long long *)T.d_nvals, gst, u.count, u.n, spmv_mode, (const X *)uhot);
             GB_LAUNCH_CHECK();
             if (A.nlchunks > 0) {
                 const unsigned fg = (unsigned)std::max<int64_t>(1, std::min<int64_t>((A.nlchunks + 255) / 256, 1024));

@@ -135,6 +135,11 @@ void gb_drop_transpose(GB_Obj *A) {
         A->pdeg[o] = nullptr;
         gb_free(A->long_tab[o]);
         A->long_tab[o] = nullptr;
+        gb_free(A->hot_ci[o]);
+        gb_free(A->hot_cols[o]);
+        A->hot_ci[o] = nullptr;
+        A->hot_cols[o] = nullptr;
+        A->hot_n[o] = 0;
         A->long_n[o] = 0;
     }
 }

@@ -82,6 +82,8 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
     const bool iso_result = gb_spmv_result_iso(sr, A->iso, uv.iso, vxm);
     if (!iso_result) gb_view_long_rows(av, A, use_csc ? 1 : 0);
     uv.full = u->kind != GB_KIND_MATRIX && u->nvals_valid && u->nvals == u->nrows && u->nrows > 0;
+    if (!iso_result && uv.full && !uv.iso && A->kind == GB_KIND_MATRIX && !gb_sr_describe(sr).positional)
+        gb_view_hot(av, A, use_csc ? 1 : 0);
     if (A->kind == GB_KIND_MATRIX && gb_knob("spmv_direction") != 1 && iso_result) {
         if (use_csc) gb_get_csr(pv, A);
         else gb_get_csc(pv, A);

@@ -458,3 +458,84 @@ void gb_transpose_csr(int64_t nrows, int64_t ncols, int64_t nvals, const int64_t
     *tcolidx = tci;
     *tvals = tvx;
 }
+
+// ---------------------------------------------------------------- hot-column relabel
+// A dense-input SpMV gathers x[k] for every entry; on a power-law matrix most entries name a
+// few columns (R-MAT s22: the 2^19 most frequent of 4.2M columns carry 93% of the entries), but
+// their x values are scattered over all of x, one 8-byte value per 128-byte line, so the
+// gathers miss in L2.  The relabel packs the hot columns' values into a contiguous array
+// (gathered once per call, 2 MB for 2^18 fp64: 85% of the s22 entries) that stays L2-resident: entries of hot columns
+// carry INT32_MIN | rank instead of the column, the rest keep their column.  Built once per
+// matrix version and orientation (freed with the other cached views).
+__global__ void k_hot_count(const int32_t *__restrict__ colidx, int64_t nvals, uint32_t *__restrict__ cnt) {
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < nvals; p += (int64_t)gridDim.x * blockDim.x)
+        atomicAdd(&cnt[colidx[p]], 1u);
+}
+
+__global__ void k_iota_i32(int32_t *__restrict__ out, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = (int32_t)i;
+}
+
+__global__ void k_hot_rank(const int32_t *__restrict__ hot, int64_t nh, int32_t *__restrict__ rank) {
+    for (int64_t h = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; h < nh; h += (int64_t)gridDim.x * blockDim.x)
+        rank[hot[h]] = (int32_t)h;
+}
+
+__global__ void k_hot_remap(const int32_t *__restrict__ colidx, int64_t nvals, const int32_t *__restrict__ rank,
+                            int32_t *__restrict__ out) {
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < nvals;
+         p += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t c = colidx[p], r = rank[c];
+        out[p] = r >= 0 ? (int32_t)((uint32_t)r | 0x80000000u) : c;
+    }
+}
+
+void gb_view_hot(gb_csr_view &v, GB_Obj *A, int orient) {
+    if (A->kind != GB_KIND_MATRIX || !v.colidx) return;
+    const int64_t knob = gb_knob("xhot");  // 0 auto, 1 never, 2 always (tests)
+    if (knob == 1) return;
+    int64_t H = gb_knob("xhot_cols");
+    if (H <= 0) H = 1LL << 18;  // 2 MB of fp64 x (tools/xhot_probe.py, s22: 2^16 684 us, 2^18 662, 2^19 667, 2^20 677)
+    if (H > v.ncols) H = v.ncols;
+    if (!A->hot_ci[orient]) {
+        // worth it only when x does not fit the L2 anyway and there is enough to gather
+        if (knob != 2 && (v.nvals < (1LL << 22) || v.ncols <= 2 * H)) return;
+        if (H <= 0 || v.nvals == 0) return;
+        const int64_t nc = v.ncols;
+        gb_scratch s;
+        uint32_t *cnt = s.get<uint32_t>(nc), *cnt2 = s.get<uint32_t>(nc);
+        int32_t *ids = s.get<int32_t>(nc), *ids2 = s.get<int32_t>(nc);
+        gb_memset(cnt, 0, nc * sizeof(uint32_t));
+        unsigned g = gb_grid(v.nvals);
+        if (g > 8192) g = 8192;
+        hipLaunchKernelGGL(k_hot_count, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), v.colidx, v.nvals, cnt);
+        GB_LAUNCH_CHECK();
+        unsigned gc = gb_grid(nc);
+        if (gc > 8192) gc = 8192;
+        hipLaunchKernelGGL(k_iota_i32, dim3(gc), dim3(GB_BLOCK), 0, gb_stream(), ids, nc);
+        GB_LAUNCH_CHECK();
+        size_t tmp = 0;
+        GB_HIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, cnt, cnt2, ids, ids2, (int)nc, 0, 32,
+                                                            gb_stream()));
+        void *tb = s.get<char>(tmp);
+        GB_HIP(hipcub::DeviceRadixSort::SortPairsDescending(tb, tmp, cnt, cnt2, ids, ids2, (int)nc, 0, 32,
+                                                            gb_stream()));
+        int32_t *hot = gb_malloc_n<int32_t>(H);
+        gb_copy_d2d(hot, ids2, H * sizeof(int32_t));
+        int32_t *rank = ids;  // reuse: -1 everywhere, then the hot ranks
+        gb_memset(rank, 0xff, nc * sizeof(int32_t));
+        hipLaunchKernelGGL(k_hot_rank, dim3(std::max(1u, std::min(gb_grid(H), 8192u))), dim3(GB_BLOCK), 0,
+                           gb_stream(), hot, H, rank);
+        GB_LAUNCH_CHECK();
+        int32_t *hci = gb_malloc_n<int32_t>(v.nvals);
+        hipLaunchKernelGGL(k_hot_remap, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), v.colidx, v.nvals, rank, hci);
+        GB_LAUNCH_CHECK();
+        A->hot_ci[orient] = hci;
+        A->hot_cols[orient] = hot;
+        A->hot_n[orient] = H;
+    }
+    v.hcolidx = A->hot_ci[orient];
+    v.hcols = A->hot_cols[orient];
+    v.nhot = A->hot_n[orient];
+}

@@ -64,7 +64,8 @@ def _msbfs(gb, A, roots, n, semiring="lor_land"):
 @pytest.mark.parametrize("direction", [0, 1, 2])  # auto (device-chosen), pull only, push only
 @pytest.mark.parametrize("hub", [0, 8])  # hub pieces of the default 512 edges, or of 8 (most rows)
 @pytest.mark.parametrize("eager", [0, 1])  # level stamps as pending layers (default) or written at once
-def test_msbfs_rmat_vs_oracle(gb, scale, k, direction, hub, eager):
+@pytest.mark.parametrize("hot", [0, 2])  # pull sources through the hot-column relabel: auto (off here) / forced
+def test_msbfs_rmat_vs_oracle(gb, scale, k, direction, hub, eager, hot):
     G = O.rmat(scale, 16, 42)
     n = G.nrows
     r, c, _ = G.to_coo()
@@ -73,7 +74,8 @@ def test_msbfs_rmat_vs_oracle(gb, scale, k, direction, hub, eager):
     deg = np.diff(G.indptr)
     roots = rng.choice(np.flatnonzero(deg > 0), k, replace=False)
     roots[0] = int(np.argmax(deg))  # the hub: long columns go to the wave path
-    with _knobs(gb, colbits=1, colbits_direction=direction, colbits_hub=hub, colbits_eager=eager):
+    with _knobs(gb, colbits=1, colbits_direction=direction, colbits_hub=hub, colbits_eager=eager,
+                xhot=hot, xhot_cols=300):
         got, _ = _msbfs(gb, A, roots, n)
     for i, src in enumerate(roots):
         lev, _, _ = O.bfs_levels(G, int(src))

@@ -882,3 +882,51 @@ def test_masked_spgemm_two_sided_vs_oracle(gb, name, mon, mul, dt, knobs, form):
         assert np.array_equal(r.astype(np.int64), er) and np.array_equal(c.astype(np.int64), ec)
     else:
         _check_mat(Cg, ref)
+
+
+@pytest.mark.parametrize("name,mon,mul,dt", [("plus_times", "PLUS", "TIMES", "FP64"),
+                                             ("plus_times", "PLUS", "TIMES", "FP32"),
+                                             ("min_plus", "MIN", "PLUS", "INT64"),
+                                             ("max_times", "MAX", "TIMES", "INT32"),
+                                             ("min_first", "MIN", "FIRST", "UINT64"),
+                                             ("plus_secondi", "PLUS", "SECONDI", "INT64")])
+@pytest.mark.parametrize("hot", [64, 1000, 3000])
+def test_spmv_hot_columns_vs_oracle(gb, name, mon, mul, dt, hot):
+    """Dense-u SpMV on the hot-column relabel (gb_prim.hip gb_view_hot; knob xhot=2 builds it at
+    any size, xhot_cols sets how many columns are hot): entries of the hot columns read the
+    packed copy of their x values.  mxv, vxm (the CSC's relabel), masked and complemented;
+    positional multipliers keep the true column.  Bit-exact for exact monoids."""
+    rng = np.random.default_rng(zlib.crc32(repr((name, dt, hot, "xhot")).encode()))
+    n = 3000
+    Ao = _skewed_csr(rng, n, dt)
+    uvals = (rng.standard_normal(n) if dt in ("FP32", "FP64") else rng.integers(0, 30, n)).astype(O.NP[dt])
+    u = O.Vec(n, dt, np.arange(n), uvals)
+    mo = _rand_csr(rng, n, 1, 0.5, "BOOL")
+    m = O.Vec.from_col(mo)
+    sr = getattr(gb.semiring, name)[dt]
+    w0 = O.Vec(n, dt, np.zeros(0, np.int64), np.zeros(0, O.NP[dt]))
+    with _knobs(gb, xhot=2, xhot_cols=hot):
+        Ag = _to_gb(gb, Ao)
+        ug = gb.Vector.from_coo(np.arange(n), uvals, dtype=dt, size=n)
+        mg = gb.Vector.from_coo(m.indices, m.values, dtype="BOOL", size=n)
+        for kind in ("mxv", "vxm", "mxv_mask", "vxm_comp"):
+            wg = gb.Vector(dt, n)
+            if kind == "mxv":
+                wg << Ag.mxv(ug, sr)
+                ref = O.mxv(w0, Ao, u, (mon, mul, dt))
+            elif kind == "vxm":
+                wg << ug.vxm(Ag, sr)
+                ref = O.vxm(w0, u, Ao, (mon, mul, dt))
+            elif kind == "mxv_mask":
+                wg(mg.V) << Ag.mxv(ug, sr)
+                ref = O.mxv(w0, Ao, u, (mon, mul, dt), mask=m)
+            else:
+                wg(~mg.S, replace=True) << ug.vxm(Ag, sr)
+                ref = O.vxm(w0, u, Ao, (mon, mul, dt), mask=m, mask_comp=True, mask_struct=True, replace=True)
+            gi, gv = wg.to_coo()
+            assert np.array_equal(gi.astype(np.int64), ref.indices), kind
+            if dt in ("FP32", "FP64") and mon == "PLUS":
+                np.testing.assert_allclose(gv, ref.values, rtol=1e-5 if dt == "FP32" else 1e-12,
+                                           atol=1e-3 if dt == "FP32" else 1e-10)
+            else:
+                assert np.array_equal(gv, ref.values), kind
