@@ -62,6 +62,8 @@ def parse():
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     # rehearsal of the N>1 path on one GPU: all ranks on one device, gloo transport
     p.add_argument("--dist-backend", default="nccl")
+    p.add_argument("--partition", default="balanced", choices=["balanced", "equal"],
+                   help="N > 1 BFS: vertex ranges balanced by the shards' entries, or equal word slots")
     p.add_argument("--device", type=int, default=None, help="override LOCAL_RANK's device")
     p.add_argument("--knob", action="append", default=[], help="library knob key=value (ablations)")
     p.add_argument("--semiring", default="any_pair", choices=["any_pair", "lor_land"],
@@ -698,6 +700,28 @@ def main():
     else:
         ok(lib.GxB_Matrix_rmat(ctypes.byref(A), scale, args.edge_factor, args.seed, 0x100, 0, lo, hi),
            "rmat shard (rows of A^T)")
+        if args.partition == "balanced":
+            # 1-D row blocks balanced by entries: the shards' per-word entry
+            # counts are all-gathered, cut into equal-entry word ranges, and each rank
+            # regenerates its shard for its range when it moved
+            ap0, _ = export_csr(lib, A, nloc)
+            wl = np.zeros(part["slot"] * 64, np.int64)
+            wl[:nloc] = np.diff(ap0)
+            xdev = "cuda" if args.dist_backend == "nccl" else "cpu"  # gloo: host tensors
+            wsum = torch.from_numpy(wl.reshape(-1, 64).sum(1)).to(xdev)
+            got = torch.zeros(part["slot"] * world, dtype=torch.int64, device=xdev)
+            dist.all_gather(list(got.chunk(world)), wsum)
+            gw = got.cpu().numpy()
+            word_nnz = np.concatenate([gw[k * part["slot"]:k * part["slot"] + (
+                gdist.partition(n, world, k)["hi_w"] - gdist.partition(n, world, k)["lo_w"])] for k in range(world)])
+            part = gdist.partition(n, world, rank, gdist.balanced_bounds(word_nnz, world))
+            if (part["lo"], part["hi"]) != (lo, hi):
+                lo_w, hi_w, lo, hi = part["lo_w"], part["hi_w"], part["lo"], part["hi"]
+                nloc = hi - lo
+                ok(lib.GrB_Matrix_free(ctypes.byref(A)), "free shard")
+                A = ctypes.c_void_p()
+                ok(lib.GxB_Matrix_rmat(ctypes.byref(A), scale, args.edge_factor, args.seed, 0x100, 0, lo, hi),
+                   "rmat balanced shard (rows of A^T)")
     torch.cuda.synchronize()
     ingest_s = time.time() - t0
     nnz_local = ctypes.c_uint64()
@@ -732,7 +756,9 @@ def main():
     nv = ctypes.c_uint64()
     ev_pairs, level_counts = [], []
 
-    zero_copy = world > 1 and part["slot"] * world == words
+    # the gathered bitmap lands in q's own device bitmap when it comes out contiguous: equal
+    # slots that tile the words exactly, or packed ranges (balanced bounds)
+    zero_copy = world > 1 and (part.get("bounds") is not None or part["slot"] * world == words)
 
     def exchange_frontier(into_q_bits):
         """all-gather the ranks' frontier slices (RCCL, on the library stream) into q"""

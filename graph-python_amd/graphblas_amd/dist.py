@@ -11,21 +11,47 @@ CPU tests).  Every rank sees the same gathered bitmap, so the termination test
 import numpy as np
 
 
-def partition(n, world, rank):
-    """Bitmap-word slot of `rank`: dict(words, slot, lo_w, hi_w, lo, hi)."""
+def partition(n, world, rank, bounds=None):
+    """Bitmap-word range of `rank`: dict(words, slot, lo_w, hi_w, lo, hi).
+
+    Default: equal slots of ceil(words / world) words.  `bounds` (world + 1 word offsets,
+    e.g. from balanced_bounds) gives unequal ranges; `slot` is then the largest range, the
+    size every rank's all-gather send buffer takes."""
     words = (n + 63) // 64
-    slot = (words + world - 1) // world
-    lo_w, hi_w = min(words, rank * slot), min(words, (rank + 1) * slot)
+    if bounds is None:
+        slot = (words + world - 1) // world
+        lo_w, hi_w = min(words, rank * slot), min(words, (rank + 1) * slot)
+    else:
+        assert len(bounds) == world + 1 and bounds[0] == 0 and bounds[-1] == words
+        slot = max(1, max(int(bounds[k + 1]) - int(bounds[k]) for k in range(world)))
+        lo_w, hi_w = int(bounds[rank]), int(bounds[rank + 1])
     return {"words": words, "slot": slot, "lo_w": lo_w, "hi_w": hi_w, "lo": lo_w * 64,
-            "hi": min(n, hi_w * 64)}
+            "hi": min(n, hi_w * 64), "bounds": None if bounds is None else [int(b) for b in bounds]}
+
+
+def balanced_bounds(word_nnz, world):
+    """Word offsets (world + 1) cutting the rows into `world` ranges of nearly equal entries
+    (1-D row blocks balanced by nnz, not rows), at 64-row word boundaries.
+    word_nnz[w] = entries of rows [64w, 64w + 64) of the sharded matrix (A^T for the pull)."""
+    c = np.concatenate([[0], np.cumsum(np.asarray(word_nnz, dtype=np.int64))])
+    words = c.size - 1
+    tot = int(c[-1])
+    b = [0]
+    for k in range(1, world):
+        w = int(np.searchsorted(c, tot * k / world, side="left"))
+        b.append(min(max(w, b[-1]), words))
+    b.append(words)
+    return b
 
 
 class BitmapAllGather:
-    """All-gather of equal-size int64 bitmap slices into one frontier bitmap.
+    """All-gather of int64 bitmap slices into one frontier bitmap.
 
     `send` (slot words) is filled by the local step (e.g. GxB_Vector_bitmap_export);
-    after `run()`, `gathered[:words]` is the full bitmap (GxB_Vector_bitmap_import).
-    Uses all_gather_into_tensor where the backend has it (NCCL/RCCL), else all_gather."""
+    after `run()`, the gathered tensor's first `words` words are the full bitmap
+    (GxB_Vector_bitmap_import).  Uses all_gather_into_tensor where the backend has it
+    (NCCL/RCCL), else all_gather.  With unequal ranges (partition(..., bounds)) every rank
+    sends `slot` words and the ranges are packed together afterwards with one index gather."""
 
     def __init__(self, dist, part, world, device):
         import torch
@@ -36,19 +62,29 @@ class BitmapAllGather:
         self.send = torch.zeros(part["slot"], dtype=torch.int64, device=device)
         self.gathered = torch.zeros(part["slot"] * world, dtype=torch.int64, device=device)
         self._fused = dist.get_backend() == "nccl"
+        self._pack = None
+        b = part.get("bounds")
+        if b is not None and any(b[k + 1] - b[k] != part["slot"] for k in range(world)):
+            # position in the gathered buffer of every word of the full bitmap
+            idx = np.concatenate([k * part["slot"] + np.arange(b[k + 1] - b[k]) for k in range(world)])
+            self._pack = torch.from_numpy(idx.astype(np.int64)).to(device)
+            self._staged = torch.zeros(part["slot"] * world, dtype=torch.int64, device=device)
 
     def run(self, out=None):
-        """Gather into `out` (e.g. a vector's device bitmap, slot*world words) or the
+        """Gather into `out` (e.g. a vector's device bitmap, at least `words` words) or the
         internal buffer; returns the tensor gathered into."""
         out = self.gathered if out is None else out
+        dst = out if self._pack is None else self._staged
         if self._fused:
-            self.dist.all_gather_into_tensor(out, self.send)
+            self.dist.all_gather_into_tensor(dst, self.send)
         elif self.send.is_cuda:  # gloo rehearsal of the GPU path: stage through host memory
-            host = torch_empty_like_cpu(out)
+            host = torch_empty_like_cpu(dst)
             self.dist.all_gather(list(host.chunk(self.world)), self.send.cpu())
-            out.copy_(host)
+            dst.copy_(host)
         else:
-            self.dist.all_gather(list(out.chunk(self.world)), self.send)
+            self.dist.all_gather(list(dst.chunk(self.world)), self.send)
+        if self._pack is not None:
+            out[:self._pack.numel()] = dst.index_select(0, self._pack)
         return out
 
 
@@ -60,13 +96,15 @@ class RowPanelAllGather:
     colidx int32[nnz_k], values [nnz_k] (or [1] when the panel is iso) -- and the blocks
     follow rank order.  run() returns the whole B (rowptr int64[n+1], colidx, values,
     iso) on every rank.  RCCL has no gatherv: the panel sizes, iso flags and iso values
-    are all-gathered first (four int64 per rank), then each owner broadcasts its panel
-    straight into its slice of the assembled buffers (no padding to the largest panel, no
-    staging copy; on the xGMI mesh every GPU receives each peer's panel over the direct
-    link) and the local row pointers are shifted by the panel's entry offset.  The result
-    is iso only when every panel is iso with the same value; otherwise iso panels are
-    expanded into their slice, so every rank issues the same collective sequence.  Issued
-    on the library stream, the result feeds GxB_Matrix_import_device."""
+    are all-gathered first (four int64 per rank); then every rank packs its panel (row
+    pointers, column indices, values: 8-byte aligned parts of one byte buffer, padded to
+    the largest panel) and ONE all-gather moves all panels at once -- on the xGMI mesh a
+    single collective keeps every link busy, where one broadcast per owner and array
+    serialises 3 x world collectives.  The panels are unpacked into the assembled buffers
+    and the local row pointers shifted by the panel's entry offset.  The result is iso only
+    when every panel is iso with the same value; otherwise iso panels are expanded into
+    their part, so every rank issues the same collective sequence.  Issued on the library
+    stream, the result feeds GxB_Matrix_import_device."""
 
     def __init__(self, dist, world, rank):
         self.dist, self.world, self.rank = dist, world, rank
@@ -88,6 +126,14 @@ class RowPanelAllGather:
         self.dist.all_gather(got, meta)
         return [tuple(int(x) for x in t) for t in torch.stack(got).cpu()]
 
+    @staticmethod
+    def _layout(nr, nnz, vsize, with_vals):
+        """Byte offsets of (row pointers, column indices, values) in a packed panel, and its size."""
+        a8 = lambda x: (x + 7) // 8 * 8  # noqa: E731
+        o_ci = a8(nr * 8)
+        o_vx = o_ci + a8(nnz * 4)
+        return o_ci, o_vx, o_vx + (a8(nnz * vsize) if with_vals else 0)
+
     def run(self, rowptr, colidx, values, iso=False):
         import torch
 
@@ -97,34 +143,54 @@ class RowPanelAllGather:
         sz = self.sizes(rowptr.numel() - 1, colidx.numel(), dev, iso, bits)
         # iso result only when all panels agree (value bits compared exactly)
         all_iso = all(s[2] for s in sz) and len({s[3] for s in sz}) == 1
+        vs = values.element_size()
         roff, eoff = [0], [0]
         for s in sz:
             roff.append(roff[-1] + s[0])
             eoff.append(eoff[-1] + s[1])
         out_rp = torch.zeros(roff[-1] + 1, dtype=torch.int64, device=dev)
         out_ci = torch.empty(eoff[-1], dtype=colidx.dtype, device=dev)
-        if all_iso:
-            out_vx = values[:1].clone()
+        out_vx = values[:1].clone() if all_iso else torch.empty(eoff[-1], dtype=values.dtype, device=dev)
+        lay = [self._layout(s[0], s[1], vs, not all_iso) for s in sz]
+        if W == 1:
+            out_rp[1:].copy_(rowptr[1:])
+            out_ci.copy_(colidx)
+            if not all_iso:
+                out_vx.copy_(values[:1].expand(out_vx.numel()) if iso else values)
+            return out_rp, out_ci, out_vx, all_iso
+        # pack this rank's panel (iso panels expanded when the result is not iso)
+        maxb = max(1, max(l[2] for l in lay))
+        o_ci, o_vx, _ = lay[r]
+        send = torch.zeros(maxb, dtype=torch.uint8, device=dev)
+        nr, nnz = sz[r][0], sz[r][1]
+        if nr:
+            send[:nr * 8].view(torch.int64).copy_(rowptr[1:])
+        if nnz:
+            send[o_ci:o_ci + nnz * 4].view(colidx.dtype).copy_(colidx)
+            if not all_iso:
+                vpart = send[o_vx:o_vx + nnz * vs].view(values.dtype)
+                vpart.copy_(values[:1].expand(nnz) if iso else values)
+        recv = torch.empty(W * maxb, dtype=torch.uint8, device=dev)
+        if self.dist.get_backend() == "nccl":
+            self.dist.all_gather_into_tensor(recv, send)
+        elif send.is_cuda:  # gloo rehearsal of the GPU path: stage through host memory
+            host = torch.empty(W * maxb, dtype=torch.uint8)
+            self.dist.all_gather(list(host.chunk(W)), send.cpu())
+            recv.copy_(host)
         else:
-            out_vx = torch.empty(eoff[-1], dtype=values.dtype, device=dev)
-            mine = out_vx[eoff[r]:eoff[r + 1]]
-            if iso:
-                mine.copy_(values[:1].expand(mine.numel()))
-            else:
-                mine.copy_(values)
-        out_rp[roff[r] + 1:roff[r + 1] + 1].copy_(rowptr[1:])
-        out_ci[eoff[r]:eoff[r + 1]].copy_(colidx)
-        if W > 1:
-            for k in range(W):
-                if sz[k][0]:
-                    self.dist.broadcast(out_rp[roff[k] + 1:roff[k + 1] + 1], src=k)
-                if sz[k][1]:
-                    self.dist.broadcast(out_ci[eoff[k]:eoff[k + 1]], src=k)
-                    if not all_iso:
-                        self.dist.broadcast(out_vx[eoff[k]:eoff[k + 1]], src=k)
+            self.dist.all_gather(list(recv.chunk(W)), send)
         for k in range(W):
-            if sz[k][0] and eoff[k]:
-                out_rp[roff[k] + 1:roff[k + 1] + 1] += eoff[k]
+            base = k * maxb
+            nr, nnz = sz[k][0], sz[k][1]
+            kc, kv, _ = lay[k]
+            if nr:
+                out_rp[roff[k] + 1:roff[k + 1] + 1].copy_(recv[base:base + nr * 8].view(torch.int64))
+                if eoff[k]:
+                    out_rp[roff[k] + 1:roff[k + 1] + 1] += eoff[k]
+            if nnz:
+                out_ci[eoff[k]:eoff[k + 1]].copy_(recv[base + kc:base + kc + nnz * 4].view(colidx.dtype))
+                if not all_iso:
+                    out_vx[eoff[k]:eoff[k + 1]].copy_(recv[base + kv:base + kv + nnz * vs].view(values.dtype))
         return out_rp, out_ci, out_vx, all_iso
 
 

@@ -37,13 +37,35 @@ def _transpose(G):
     return _Csr(indptr, rows[order])
 
 
-def _worker(rank, world, port, scale, src, out_q):
+def _degree_sorted(G):
+    """G relabelled so vertex ids fall with out-degree: hubs first, the unscrambled layout of
+    real graphs for which equal vertex slots are badly unbalanced."""
+    order = np.argsort(-np.diff(G.indptr), kind="stable")
+    new = np.empty_like(order)
+    new[order] = np.arange(order.size)
+    rows = new[np.repeat(np.arange(G.nrows), np.diff(G.indptr))]
+    return O.Csr.from_coo(rows, new[G.indices], np.ones(rows.size, bool), nrows=G.nrows, ncols=G.ncols,
+                          dtype="BOOL")
+
+
+def _graph(scale, skewed):
+    G = O.rmat(scale, 16, 42)
+    return _degree_sorted(G) if skewed else G
+
+
+def _worker(rank, world, port, scale, src, out_q, balanced=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    G = O.rmat(scale, 16, 42)
+    G = _graph(scale, balanced)
     n = G.nrows
     AT = _transpose(G)  # rows of A^T = in-edges: pull mxv, as in bench.py
-    part = gdist.partition(n, world, rank)
+    bounds = None
+    if balanced:  # 1-D row blocks balanced by the shard's entries (SURVEY §8(e))
+        words = (n + 63) // 64
+        deg = np.zeros(words * 64, np.int64)
+        deg[:n] = np.diff(AT.indptr)
+        bounds = gdist.balanced_bounds(deg.reshape(words, 64).sum(1), world)
+    part = gdist.partition(n, world, rank, bounds)
     lo, hi = part["lo"], part["hi"]
     ex = gdist.BitmapAllGather(dist, part, world, "cpu")
     frontier = np.zeros(n, bool)
@@ -65,12 +87,14 @@ def _worker(rank, world, port, scale, src, out_q):
             nxt[r - lo] = bool(frontier[cols].any())
         ex.send.copy_(torch.from_numpy(gdist.pack_bits(nxt, part["slot"])))
         full = ex.run().numpy()
-        # words are slot-aligned per rank: rank k's slice starts at word k*slot
-        frontier = np.zeros(n, bool)
-        for k in range(world):
-            pk = gdist.partition(n, world, k)
-            sl = full[k * part["slot"]:k * part["slot"] + (pk["hi_w"] - pk["lo_w"])]
-            frontier[pk["lo"]:pk["hi"]] = gdist.unpack_bits(sl, pk["hi"] - pk["lo"])
+        if bounds is not None:  # ranges packed together: the whole bitmap
+            frontier = gdist.unpack_bits(full[:part["words"]], n)
+        else:  # words are slot-aligned per rank: rank k's slice starts at word k*slot
+            frontier = np.zeros(n, bool)
+            for k in range(world):
+                pk = gdist.partition(n, world, k)
+                sl = full[k * part["slot"]:k * part["slot"] + (pk["hi_w"] - pk["lo_w"])]
+                frontier[pk["lo"]:pk["hi"]] = gdist.unpack_bits(sl, pk["hi"] - pk["lo"])
         if not frontier.any():
             break
     out_q.put((rank, lo, hi, level))
@@ -78,16 +102,16 @@ def _worker(rank, world, port, scale, src, out_q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("scale", [8, 10])
-def test_sharded_bfs_world2_matches_oracle(scale):
-    world = 2
-    G = O.rmat(scale, 16, 42)
+@pytest.mark.parametrize("scale,world,balanced", [(8, 2, False), (10, 2, False), (10, 2, True), (9, 3, True)])
+def test_sharded_bfs_world2_matches_oracle(scale, world, balanced):
+    G = _graph(scale, balanced)
     src = int(np.argmax(np.diff(G.indptr)))
     ref, _, _ = O.bfs_levels(G, src)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, scale, src, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, scale, src, q, balanced))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = np.zeros(G.nrows, np.int32)
@@ -109,3 +133,29 @@ def test_partition_covers_vertices():
                 covered[p["lo"]:p["hi"]] += 1
                 assert p["lo"] % 64 == 0 and p["hi_w"] - p["lo_w"] <= p["slot"]
             assert (covered == 1).all()
+
+
+def test_balanced_bounds_even_out_a_skewed_graph():
+    """On a degree-sorted graph equal vertex slots put most entries on rank 0; nnz-balanced
+    word ranges keep every rank within a few words' entries of the mean."""
+    G = _degree_sorted(O.rmat(12, 16, 42))
+    n = G.nrows
+    words = (n + 63) // 64
+    deg = np.zeros(words * 64, np.int64)
+    deg[:n] = np.diff(G.indptr)
+    wn = deg.reshape(words, 64).sum(1)
+    for world in (2, 3, 8):
+        b = gdist.balanced_bounds(wn, world)
+        assert b[0] == 0 and b[-1] == words and all(b[k] <= b[k + 1] for k in range(world))
+        per = [int(wn[b[k]:b[k + 1]].sum()) for k in range(world)]
+        eq = [int(wn[gdist.partition(n, world, k)["lo_w"]:gdist.partition(n, world, k)["hi_w"]].sum())
+              for k in range(world)]
+        mean = wn.sum() / world
+        assert max(per) <= mean + wn.max()
+        assert max(eq) > 1.5 * mean  # what the equal slots would have done
+        parts = [gdist.partition(n, world, k, b) for k in range(world)]
+        covered = np.zeros(n, int)
+        for p in parts:
+            covered[p["lo"]:p["hi"]] += 1
+            assert p["hi_w"] - p["lo_w"] <= p["slot"]
+        assert (covered == 1).all()

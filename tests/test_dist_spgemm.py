@@ -1,7 +1,7 @@
 """Row-sharded SpGEMM exchange at world_size 2 and 3 on CPU (gloo): each rank holds a
 consecutive block of rows of A (= its panel of B, since C = A*A); the CSR row panels
-are all-gathered (graphblas_amd.dist.RowPanelAllGather: sizes, then one broadcast per
-owner straight into the assembled buffers) and the local product C_r = A_r plus.times B
+are all-gathered (graphblas_amd.dist.RowPanelAllGather: sizes, then one all-gather of
+the packed panels) and the local product C_r = A_r plus.times B
 (here the oracle; GrB_mxm on the GPU, bench.py config 5) stacked over the ranks must
 equal the oracle's A plus.times A.  SURVEY §8(e) mxm row; DESIGN.md §6."""
 import os
@@ -87,6 +87,9 @@ def test_row_panel_world1_and_iso():
 
         def broadcast(self, t, src):
             raise AssertionError("no broadcast at world 1")
+
+        def get_backend(self):
+            raise AssertionError("no panel collective at world 1")
 
     G = O.rmat(7, 8, 42, values="FP64", value_seed=2)
     rp = torch.from_numpy(G.indptr.copy())
