@@ -1188,12 +1188,12 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
         push = gb_dir_decide(mf, a.rule);
     }
     else if (a.dst) push = a.dst[ST_PUSH] != 0;
-    if (a.spare) {
+    if (a.spare && !(a.dbg & 32)) {  // dbg 32: diagnostics, no zeroing
         for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < a.spare_words;
              w += (int64_t)gridDim.x * blockDim.x)
             a.spare[w] = 0;
     }
-    for (int j = 0; j < a.nzb; j++)  // cleared vectors' bitmaps, back to the pool zeroed
+    for (int j = 0; j < ((a.dbg & 32) ? 0 : a.nzb); j++)  // cleared vectors' bitmaps, back to the pool zeroed
         for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < a.zb_words;
              w += (int64_t)gridDim.x * blockDim.x)
             a.zb[j][w] = 0;
@@ -1213,6 +1213,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
         cnt = gb_pull_iso_phase(nrows, rowptr, colidx, ubits, mbits, mcomp, tbits, L, a.hprow, mfn, a.p1_steps,
                                 a.cap0, a.rows_nonempty, qbits, a.asg, adelta, a.dbg,
                                 (a.phead && (!a.hprow || a.pdeg)) ? a.phead : nullptr, a.pdeg);
+    if (a.dbg & 64) return;  // diagnostics: no finish (count, hint, mailbox)
     if (a.packed) {
         iso_finish_packed(cnt, mfn, adelta, tcount, gst, a);
         return;
