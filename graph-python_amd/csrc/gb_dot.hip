@@ -38,9 +38,9 @@ namespace {
 constexpr int DT_BLOCK = 256;
 constexpr int DT_SMALL = 64;      // long side <= 64: k_dot_small, keys one per lane
 constexpr int DT_MID = 256;       // long side <= 256: k_dot_small, four keys per lane
-constexpr int DT_CAP = 16384;     // long side <= DT_CAP: k_dot_task (keys in LDS)
+constexpr int DT_CAP = 8192;      // long side <= DT_CAP: k_dot_task (keys in LDS)
 constexpr int DT_OVH = 256;       // per-entry cost added to the streamed length (task windows)
-constexpr int DT_WIN = 65536;     // task window: <= DT_WIN / DT_OVH entries start in one
+constexpr int DT_WIN = 32768;     // task window: <= DT_WIN / DT_OVH entries start in one
 constexpr int DT_MAXE = DT_WIN / DT_OVH;
 
 static inline unsigned dt_grid(int64_t n, int per_block = DT_BLOCK, int64_t cap = 1 << 16) {
@@ -370,11 +370,11 @@ __global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, dt_side s, const 
 //     (a lane's staged elements come in entry order) and meet per entry in LDS
 //     slots (atomic fold of an exact monoid, one per lane run -- one per wave when
 //     the wave's hits share an entry), written to T at the end of the task.
-constexpr int DT_TB = 1024;      // task workgroup: 16 waves, one workgroup per CU
-constexpr int DT_U = 8;          // 64-element windows per step (loads in flight per lane)
+constexpr int DT_TB = 1024;      // task workgroup: 16 waves, two workgroups per CU (74.8 KB LDS, <= 64 VGPRs)
+constexpr int DT_U = 4;          // 64-element windows per step (loads in flight per lane)
 constexpr int DT_PIECE = 1024;   // elements per unit (a multiple of 64 * DT_U)
 constexpr int DT_SMAX = DT_WIN + DT_CAP;  // flat elements per task bound
-constexpr int DT_FLOG = 18;      // filter bits (log2)
+constexpr int DT_FLOG = 17;      // filter bits (log2)
 
 __device__ __forceinline__ uint32_t dt_hash(int32_t k) { return ((uint32_t)k * 0x9E3779B1u) >> (32 - DT_FLOG); }
 
@@ -428,7 +428,9 @@ __device__ __forceinline__ void dt_slot_fold(const SR &sr, bool any_store, unsig
 }
 
 template <class SR, class X, class Z, bool SWAP>
-__global__ __launch_bounds__(DT_TB) void k_dot_task(
+// 8 waves per SIMD: two workgroups per CU (round 3: one workgroup of 149.6 KB LDS and 78 VGPRs
+// per CU left the latency-bound stream at 4 waves per SIMD; s22 128 -> 117 ms, s20 27.2 -> 23.5)
+__global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
     SR sr, int mon, dt_side s, const X *__restrict__ xvx, bool x_iso, const X *__restrict__ yvx, bool y_iso,
     int64_t ntask, const int64_t *__restrict__ tstart, const int32_t *__restrict__ eG,
     const int64_t *__restrict__ eYS, const int32_t *__restrict__ eO, const int32_t *__restrict__ eB,
