@@ -560,7 +560,7 @@ __device__ __forceinline__ int64_t gallop_lb(const int32_t *__restrict__ ci, int
 }
 
 constexpr int WEG = 512;  // A entries per sweep group of the window kernels
-constexpr int WP = 4;     // products per thread per tile of the window kernels
+constexpr int WP = 2;     // products per thread per tile of the window kernels
 
 // The products of row i with columns in [cursor, cend) are enumerated WEG A entries at a
 // time: win_entries finds every entry's end of range, win_tiles hands WP products per thread
@@ -711,7 +711,7 @@ __device__ __forceinline__ int32_t win_sweep(win_sweep_lds &L, int64_t a0, int64
 // Symbolic (SYM: distinct columns per row) and key-only numeric (the window's set bits
 // written out in column order: C's colidx comes out sorted).
 template <bool SYM, class SR, class X, class Z>
-__global__ __launch_bounds__(HG) void k_row_window(
+__global__ __launch_bounds__(HG, 8) void k_row_window(
     SR sr, const int32_t *__restrict__ rows, int64_t nr, int logW, int64_t *__restrict__ cur,
     const int64_t *__restrict__ arp, const int32_t *__restrict__ aci, const int64_t *__restrict__ brp,
     const int32_t *__restrict__ bci, int64_t ncols, int64_t *__restrict__ cnt, const int64_t *__restrict__ crp,
@@ -820,7 +820,7 @@ __global__ __launch_bounds__(HG) void k_row_window(
 // group (LDS slots of < vcap entries, one sweep each) or, past in_c_groups groups, in one
 // sweep straight into C's values.  DET: the slots are owned by waves (msplit above).
 template <bool DET, class SR, class X, class Z>
-__global__ __launch_bounds__(HG) void k_window_num(
+__global__ __launch_bounds__(HG, 8) void k_window_num(
     SR sr, int mon, const int32_t *__restrict__ rows, int64_t nr, int logW, int vcap, int in_c_groups,
     int64_t *__restrict__ cur, const int64_t *__restrict__ arp, const int32_t *__restrict__ aci,
     const X *__restrict__ avx, bool a_iso, const int64_t *__restrict__ brp, const int32_t *__restrict__ bci,
@@ -1261,8 +1261,11 @@ void spgemm_hash_run(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, const gb_
             // values; one-to-two-byte values: a group can hold the whole window)
             // narrow values: at least 512 columns, so a value group (vcap - 256 entries,
             // one 256-column chunk of headroom) is never empty
-            const int lw = SYM ? win_log(19) : (sizeof(Z) < 4 ? std::max(9, win_log(13)) : win_log(17));
-            int vcap = (SYM || !VALS) ? 0 : (sizeof(Z) < 4 ? (1 << lw) : 8192);
+            // numeric windows sized for two 1024-thread workgroups per CU (round 3: 2^17 columns,
+            // 8192 LDS values and 4 products per thread held one workgroup of 153 KB LDS per
+            // CU at 4 waves per SIMD; config 5 s19 219 -> 204 ms at 2^16 / 3072 / 2, <= 64 VGPRs)
+            const int lw = SYM ? win_log(19) : (sizeof(Z) < 4 ? std::max(9, win_log(13)) : win_log(16));
+            int vcap = (SYM || !VALS) ? 0 : (sizeof(Z) < 4 ? (1 << lw) : 3072);
             // tests: a small LDS value capacity sends windows to the C-resident accumulation
             const int64_t kv = gb_knob("window_vcap");
             if (vcap && kv > 256 && kv < vcap) vcap = (int)kv;
