@@ -74,6 +74,8 @@ def parse():
     p.add_argument("--spgemm-steps", type=int, default=2)
     p.add_argument("--spgemm-warmup", type=int, default=1)
     p.add_argument("--no-spgemm", action="store_true", help="skip the config 5 line")
+    p.add_argument("--spgemm-scale-big", type=int, default=20,
+                   help="N = 1: a second config 5 line at this scale (the largest that fits one GPU); 0 skips")
     return p.parse_args()
 
 
@@ -963,6 +965,12 @@ def main():
         secondary.update(secondary_workloads(lib, torch, stream, O, args))
     if not args.no_spgemm:
         secondary["config5_spgemm_plus_times_fp64"] = config5_spgemm(lib, torch, stream, dist, world, rank, args)
+        if world == 1 and args.spgemm_scale_big > args.spgemm_scale:
+            # the largest unmasked scale that fits one GPU (s20: C has 9.7e9 entries, 116 GB)
+            big = argparse.Namespace(**vars(args))
+            big.spgemm_scale = args.spgemm_scale_big
+            secondary[f"config5_spgemm_plus_times_fp64_s{big.spgemm_scale}"] = config5_spgemm(
+                lib, torch, stream, dist, world, rank, big)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -720,10 +720,11 @@ struct gb_iso_args {
 template <class SR, class X, class Z, bool FLIP>
 __device__ __forceinline__ void gb_spmv_product(SR &sr, bool rv, const X *__restrict__ avals, bool a_iso, X a0,
                                                 const X *__restrict__ uvals, bool u_iso, X u0, int64_t p, int k,
-                                                int64_t r, Z &z, const X *__restrict__ uhot) {
+                                                int64_t r, Z &z, const X *__restrict__ uhot, bool nt = false) {
     X a = X(), b = X();
     if (rv) {
-        a = a_iso ? a0 : avals[p];
+        // nt: the streamed A values bypass L2 retention (the hot x values stay resident)
+        a = a_iso ? a0 : (nt ? __builtin_nontemporal_load(&avals[p]) : avals[p]);
         // k < 0: a hot column (relabelled colidx, gb_view_hot): its value from the packed copy
         b = u_iso ? u0 : (k < 0 ? uhot[k & 0x7fffffff] : uvals[k]);
     }
@@ -924,6 +925,8 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
     }
     // u has every entry: no presence tests (a relabelled colidx, uhot, is used only then)
     const bool ufull = uhot || (ucount && *ucount == un);
+    const bool nt = (mode & 2) != 0;  // non-temporal loads of the streamed colidx / values
+    mode &= 1;
     fl[lane] = 0;
     gb_wave_sync();
     long long cnt = 0;
@@ -942,14 +945,14 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
                     ok[u] = q + 64 * u < p1;
-                    kk[u] = ok[u] ? colidx[q + 64 * u] : 0;
+                    kk[u] = ok[u] ? (nt ? __builtin_nontemporal_load(&colidx[q + 64 * u]) : colidx[q + 64 * u]) : 0;
                 }
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
                     if (!ok[u] || (!ufull && !gb_bit(ubits, kk[u]))) continue;
                     Z t;
                     gb_spmv_product<SR, X, Z, FLIP>(sr, rv, avals, a_iso, a0, uvals, u_iso, u0, q + 64 * u, kk[u],
-                                                    r, t, uhot);
+                                                    r, t, uhot, nt);
                     z = f ? sr.add(z, t) : t;
                     f = true;
                 }
@@ -1010,7 +1013,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
                 own[u] = lo;
                 pos[u] = __shfl(p0, lo, 64) + (e - __shfl(excl, lo, 64));
                 ok[u] = e < total;
-                k[u] = ok[u] ? colidx[pos[u]] : 0;
+                k[u] = ok[u] ? (nt ? __builtin_nontemporal_load(&colidx[pos[u]]) : colidx[pos[u]]) : 0;
             }
             bool fu[SPMV_WU];
             Z zu[SPMV_WU];
@@ -1020,7 +1023,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
                 zu[u] = Z();
                 if (fu[u])
                     gb_spmv_product<SR, X, Z, FLIP>(sr, rv, avals, a_iso, a0, uvals, u_iso, u0, pos[u], k[u],
-                                                    (w << 6) + own[u], zu[u], uhot);
+                                                    (w << 6) + own[u], zu[u], uhot, nt);
             }
 #pragma unroll
             for (int u = 0; u < SPMV_WU; u++) {
@@ -1665,7 +1668,8 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             int8_t *cfound = s.get<int8_t>(A.nlchunks + 1);
             const int64_t units = std::max<int64_t>(nw, A.nlchunks);
             const bool u_iso_k = u.iso || gb_knob("spmv_timing_no_x_gather") == 1;  // timing experiment only
-            const int spmv_mode = gb_knob("spmv_words") == 2 ? 1 : 0;  // 0: segmented scan (default), 2: merge path
+            int spmv_mode = gb_knob("spmv_words") == 2 ? 1 : 0;  // 0: segmented scan (default), 2: merge path
+            if (gb_knob("spmv_nt") == 1) spmv_mode |= 2;
             const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 3) / 4, 4096));
             // dense u on a relabelled matrix: the hot columns' values packed first (gb_view_hot);
             // positional multipliers need the true column, so they keep the plain colidx
