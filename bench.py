@@ -59,7 +59,7 @@ def parse():
     p.add_argument("--no-msbfs", action="store_true", help="skip the multi-source (masked mxm) BFS line")
     p.add_argument("--msbfs-sharded", action="store_true", help="N > 1: add the row-sharded multi-source BFS line")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
-    p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
+    p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
     # rehearsal of the N>1 path on one GPU: all ranks on one device, gloo transport
     p.add_argument("--dist-backend", default="nccl")
     p.add_argument("--partition", default="balanced", choices=["balanced", "equal"],
