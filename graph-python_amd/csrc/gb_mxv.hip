@@ -1511,7 +1511,9 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
     const int64_t dir_knob = gb_knob("spmv_direction");  // 0 auto, 1 pull only, 2 push only
     const bool can_push = iso && Apush && Apush->nrows == u.n && Apush->hubs && dir_knob != 1;
     int64_t alpha = gb_knob("push_alpha");
-    if (alpha <= 0) alpha = 14;
+    // Beamer's alpha, swept with tools/ab_bfs.py (s22, 16 roots, 8 interleaved rounds; two boxes):
+    // 14 -> 0.312 / 0.328 ms per BFS, 36 -> 0.299 / 0.318, 48 -> 0.2985, 64 -> 0.314, 96 -> 0.323
+    if (alpha <= 0) alpha = 48;
     const int64_t nw = gb_words(n);
     unsigned long long *gst = gb_device_state();
     unsigned long long *dst = gst + GB_DIR_STATE_OFFSET;
