@@ -1158,17 +1158,18 @@ __device__ __forceinline__ void iso_finish_packed(long long cnt, long long mfn, 
     const unsigned long long o2 =
         atomicAdd(root, (sadd << (ISO_ARR_BITS + ISO_VAL_BITS)) | (scnt << ISO_ARR_BITS) | 1ULL);
     if ((unsigned)(o2 & AM) + 1 != nshards) return;
-    atomicExch(root, 0ULL);
     const long long tot = (long long)(((o2 >> ISO_ARR_BITS) & VM) + scnt);
     const long long add = (long long)((o2 >> (ISO_ARR_BITS + ISO_VAL_BITS)) + sadd);
     *tcount = (unsigned long long)tot;
-    if (a.asg.bits && add) atomicAdd(a.asg_count, (unsigned long long)add);
-    if (a.iso_out) gb_iso_eval(a.mul, a.xcode, a.zcode, a.flip, a.a0, a.u0, a.iso_out);
     if (a.pub && !(a.dbg & 1)) {  // hand the count to the host without a copy (gb_host_slot_wait)
         __hip_atomic_store(&a.pub->value, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __threadfence_system();
         __hip_atomic_store(&a.pub->seq, a.pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    // after the publish (off the host's critical path; the next launch on the stream starts
+    // only after this kernel has ended): the root reset and the fused assign's count
+    atomicExch(root, 0ULL);
+    if (a.asg.bits && add) atomicAdd(a.asg_count, (unsigned long long)add);
 }
 
 // One launch does the chosen direction and finishes the result: count
@@ -1203,6 +1204,9 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
     if (blockIdx.x == 0)
         for (int j = 0; j < a.nzc; j++)
             for (int w = threadIdx.x; w < 2 + GB_HINT_PARTS; w += blockDim.x) a.zc[j][w] = 0;
+    // the result's iso value does not depend on the work: evaluated here, off the finish's path
+    if (a.packed && a.iso_out && blockIdx.x == 0 && threadIdx.x == 0)
+        gb_iso_eval(a.mul, a.xcode, a.zcode, a.flip, a.a0, a.u0, a.iso_out);
     // fused assign: q's value mask is empty when q is iso with a false value
     const uint64_t *qbits = nullptr;
     if (a.asg.bits && (!a.asg_qiso || gb_dyn_nonzero(a.asg_qiso, a.asg_qiso_code))) qbits = ubits;
