@@ -467,6 +467,7 @@ struct gb_asg {
     const void *q_iso = nullptr;  // q's iso value when q is a value mask (nullptr: structure)
     int q_iso_code = -1;
     int64_t *count = nullptr;  // w's device count
+    int64_t h_count = -1;      // w's count before the assign, when the host knew it (-1: not known)
 };
 void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, gb_bitmap_view &u,
              const gb_vmask &mask, GrB_Semiring sr, bool flip, const gb_asg *asg = nullptr);

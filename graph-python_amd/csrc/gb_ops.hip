@@ -77,6 +77,10 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
     gb_make_vmask(m, mask, d, a_rows);
     // an empty mask vector: its count is known on the host (value or structure alike)
     if (m.bits && mask && mask->kind != GB_KIND_MATRIX && mask->nvals_valid && mask->nvals == 0) m.h_count = 0;
+    // the fused assign's target is the mask (take_pending_assign): its count before this call's
+    // assign, as the host knew it when the assign was deferred (a BFS's first level after
+    // clearing v: 0), lets gb_spmv pick push on the host without the prep launch
+    if (fused && m.bits && m.h_count < 0 && asg.h_count >= 0) m.h_count = asg.h_count;
     // the other orientation (cached on matrices) enables the push direction for iso results
     const gb_csr_view *push = nullptr;
     const bool iso_result = gb_spmv_result_iso(sr, A->iso, uv.iso, vxm);
@@ -608,6 +612,7 @@ static struct {
     GB_Obj *w = nullptr, *mask = nullptr;
     char x[16];
     gb_desc d;
+    int64_t w_count = -1;  // w's count before the deferral, when the host knew it
 } g_pend;
 
 // A failure of the deferred assign is an execution error of `w`, not of the call that
@@ -646,6 +651,7 @@ static bool try_defer_assign(GB_Obj *w, GB_Obj *mask, const char *xc, const gb_d
     g_pend.mask = mask;
     memcpy(g_pend.x, xc, sizeof(g_pend.x));
     g_pend.d = d;
+    g_pend.w_count = w->nvals_valid ? w->nvals : -1;
     g_pending_active.store(true, std::memory_order_release);
     w->nvals_valid = false;
     w->hint_valid = false;
@@ -667,6 +673,7 @@ static bool take_pending_assign(gb_asg &asg, GB_Obj *w, GB_Obj *mask, GB_Obj *A,
     asg.q_iso = g_pend.d.structure ? nullptr : u->dense;
     asg.q_iso_code = u->type->code;
     asg.count = pw->d_nvals;
+    asg.h_count = g_pend.w_count;
     g_pend.w = g_pend.mask = nullptr;
     g_pending_active.store(false, std::memory_order_release);
     return true;
