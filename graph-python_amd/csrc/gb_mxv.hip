@@ -1029,19 +1029,26 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_spmv_words(
             for (int u = 0; u < SPMV_WU; u++) {
                 bool f = fu[u];
                 Z z = zu[u];
-                // segmented inclusive scan over lanes of the same row
+                // segmented inclusive scan over lanes of the same row; the segments and the
+                // products' presence travel as two ballots, so each step shuffles only z:
+                // before step off, lane l holds [max(seg, l-off+1), l]
                 const int row = ok[u] ? own[u] : 64 + lane;  // idle lanes: own segment
+                const int prow = __shfl_up(row, 1, 64);  // all lanes shuffle (not under ||)
+                const unsigned long long heads = __ballot(lane == 0 || prow != row);
+                const unsigned long long fmask = __ballot(f);
+                const int seg = 63 - __clzll(heads & ((2ULL << lane) - 1ULL));  // this row's first lane
                 for (int off = 1; off < 64; off <<= 1) {
-                    const int orow = __shfl_up(row, off, 64);
-                    const bool of = __shfl_up((int)f, off, 64);
                     const Z oz = gb_shfl_up(z, off, 64);
-                    if (lane >= off && orow == row && of) {
-                        z = f ? sr.add(oz, z) : oz;
-                        f = true;
+                    const int hi = lane - off;
+                    if (hi >= seg) {
+                        const int lo = hi - off + 1 > seg ? hi - off + 1 : seg;
+                        if ((fmask >> lo) & ((2ULL << (hi - lo)) - 1ULL)) {  // lane hi's range holds a product
+                            z = f ? sr.add(oz, z) : oz;
+                            f = true;
+                        }
                     }
                 }
-                const int nrow = __shfl_down(row, 1, 64);
-                const bool last = ok[u] && (lane == 63 || nrow != row);
+                const bool last = ok[u] && (lane == 63 || ((heads >> (lane + 1)) & 1ULL));
                 // a row's runs arrive in order (earlier batches first): fold into its accumulator
                 if (last && f) {
                     acc[row] = fl[row] ? sr.add(acc[row], z) : z;
