@@ -1655,6 +1655,14 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             args.zb_words = g_zp_words;
             args.nzc = (int)std::min<size_t>(g_zp_dirty_c.size(), GB_ZP_MAX);
             for (int j = 0; j < args.nzc; j++) args.zc[j] = g_zp_dirty_c[j];
+            if (args.dbg & (8 | 32)) {
+                // diagnostics that return before (8) or skip (32) the zeroing: nothing handed to this
+                // launch may be treated as zeroed afterwards
+                args.nzb = args.nzc = 0;
+                if (args.spare) gb_free(args.spare);
+                args.spare = nullptr;
+                args.spare_words = 0;
+            }
             int64_t gcap = gb_knob("iso_work_grid");
             if (gcap <= 0) gcap = iso_work_resident_blocks();
             const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 3) / 4, gcap));

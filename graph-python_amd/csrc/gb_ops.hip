@@ -80,7 +80,10 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
     // the fused assign's target is the mask (take_pending_assign): its count before this call's
     // assign, as the host knew it when the assign was deferred (a BFS's first level after
     // clearing v: 0), lets gb_spmv pick push on the host without the prep launch
-    if (fused && m.bits && m.h_count < 0 && asg.h_count >= 0) m.h_count = asg.h_count;
+    // -- a stored-entry count equals the set-bit count only for a structural mask; for a value
+    // mask it is an upper bound, which still bounds the open rows of a complemented mask from
+    // below but says nothing for a plain one
+    if (fused && m.bits && m.h_count < 0 && asg.h_count >= 0 && (d.structure || d.comp)) m.h_count = asg.h_count;
     // the other orientation (cached on matrices) enables the push direction for iso results
     const gb_csr_view *push = nullptr;
     const bool iso_result = gb_spmv_result_iso(sr, A->iso, uv.iso, vxm);
@@ -1086,8 +1089,19 @@ GrB_Info GrB_Vector_assign(GrB_Vector w, const GrB_Vector mask, const GrB_Binary
         gb_bitmap_count(T.bits, n, T.d_nvals);
         GrB_Vector tv = (GrB_Vector)Tv;
         GrB_Vector_free(&tv);
-        if (!accum) vector_clear_region(W, L, gb_obj_check(mask, true), d);
-        gb_writeback_vector(W, T, gb_obj_check(mask, true), d, accum ? accum : second_of(W->type->code), false);
+        GB_Obj *Mo = gb_obj_check(mask, true);
+        // w(w.S)[I] = u / w(w.V)[I] = u: the region clear below edits w's bitmap, which IS the
+        // mask; the writeback must see the mask as it was before the clear, so take a copy
+        struct mask_copy {
+            GrB_Vector h = nullptr;
+            ~mask_copy() { if (h) GrB_Vector_free(&h); }
+        } mc;
+        if (!accum && Mo == W) {
+            GB_REQUIRE(GrB_Vector_dup(&mc.h, mask) == GrB_SUCCESS, GrB_OUT_OF_MEMORY, "mask copy");
+            Mo = gb_obj_check(mc.h);
+        }
+        if (!accum) vector_clear_region(W, L, Mo, d);
+        gb_writeback_vector(W, T, Mo, d, accum ? accum : second_of(W->type->code), false);
     });
 }
 

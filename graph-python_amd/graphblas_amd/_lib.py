@@ -18,11 +18,15 @@ from . import _builtins
 # library is loaded first, its DT_NEEDED pulls /opt/rocm's runtime in and torch's later CUDA
 # init finds "no ROCm-capable device"; importing torch first makes the dynamic loader resolve
 # our libamdhip64.so.7 to the runtime torch already loaded (bench.py, the device views and the
-# RCCL exchange all share torch's stream / device with the library).
-try:  # torch is optional (plumbing only)
-    import torch  # noqa: F401
-except Exception:
-    pass
+# RCCL exchange all share torch's stream / device with the library).  torch's bundled runtime
+# (ROCm 7.0 wheel, soname libamdhip64.so.7) is ABI-compatible with the ROCm 7.2 the library is
+# built against; a process that never uses torch can skip the import (and its seconds of start-up)
+# with GRAPHBLAS_AMD_TORCH=0, after which it must not import torch's GPU side either.
+if os.environ.get("GRAPHBLAS_AMD_TORCH", "1") != "0":
+    try:  # torch is optional (plumbing only)
+        import torch  # noqa: F401
+    except Exception:
+        pass
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GRAPHBLAS_AMD_LIB", os.path.join(_HERE, "libgraphblas_amd.so"))
@@ -73,6 +77,12 @@ _SIGS = {
     "GxB_Vector_bitmap_export": [P, P, I], "GxB_Vector_bitmap_import": [P, P, I],
     "GxB_Matrix_import_device": [P, P, I, I, P, P, P, I, ctypes.c_bool],
     "GxB_Matrix_colwords_view": [P, P, P], "GxB_Matrix_colwords_touch": [P],
+    # GrB_Scalar-argument variants (gb_scalar_args.cpp)
+    "GrB_Vector_extractElement_Scalar": [P, P, I], "GrB_Matrix_extractElement_Scalar": [P, P, I, I],
+    "GrB_Vector_setElement_Scalar": [P, P, I], "GrB_Matrix_setElement_Scalar": [P, P, I, I],
+    "GrB_Vector_assign_Scalar": [P, P, P, P, P, I, P], "GrB_Matrix_assign_Scalar": [P, P, P, P, P, I, P, I, P],
+    "GrB_Vector_apply_BinaryOp1st_Scalar": [P] * 7, "GrB_Vector_apply_BinaryOp2nd_Scalar": [P] * 7,
+    "GrB_Matrix_apply_BinaryOp1st_Scalar": [P] * 7, "GrB_Matrix_apply_BinaryOp2nd_Scalar": [P] * 7,
 }
 for _t in TYPE_NAMES:
     _T = _CTYPES[_t]

@@ -264,6 +264,41 @@ GrB_Info GrB_Scalar_free(GrB_Scalar *s);
 GrB_Info GrB_Scalar_wait(GrB_Scalar s, GrB_WaitMode mode);
 GrB_Info GrB_Scalar_error(const char **error, const GrB_Scalar s);
 
+/* GrB_Scalar-argument variants (C API 2.0; python-graphblas calls them for non-C scalars):
+ * extractElement: reference core/vector.py:1769, core/matrix.py:2837 -- a missing entry leaves
+ *   s empty and returns GrB_SUCCESS;
+ * setElement: core/vector.py:1808, core/matrix.py:2902 -- an empty x deletes the entry;
+ * assign: core/vector.py:1918,1939, core/matrix.py:3279,3305 -- an empty x assigns "no value"
+ *   (the selected part of the region is deleted; left alone under accum);
+ * apply_BinaryOp1st/2nd: core/vector.py:1406,1449, core/matrix.py:2392,2435 -- an empty x is
+ *   GrB_EMPTY_OBJECT. */
+GrB_Info GrB_Vector_extractElement_Scalar(GrB_Scalar s, const GrB_Vector v, GrB_Index i);
+GrB_Info GrB_Matrix_extractElement_Scalar(GrB_Scalar s, const GrB_Matrix A, GrB_Index i, GrB_Index j);
+GrB_Info GrB_Vector_setElement_Scalar(GrB_Vector w, const GrB_Scalar x, GrB_Index i);
+GrB_Info GrB_Matrix_setElement_Scalar(GrB_Matrix C, const GrB_Scalar x, GrB_Index i, GrB_Index j);
+GrB_Info GrB_Vector_assign_Scalar(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum,
+                                  const GrB_Scalar x, const GrB_Index *I, GrB_Index ni,
+                                  const GrB_Descriptor desc);
+GrB_Info GrB_Matrix_assign_Scalar(GrB_Matrix C, const GrB_Matrix Mask, const GrB_BinaryOp accum,
+                                  const GrB_Scalar x, const GrB_Index *I, GrB_Index ni,
+                                  const GrB_Index *J, GrB_Index nj, const GrB_Descriptor desc);
+GrB_Info GrB_Vector_apply_BinaryOp1st_Scalar(GrB_Vector w, const GrB_Vector mask,
+                                             const GrB_BinaryOp accum, const GrB_BinaryOp op,
+                                             const GrB_Scalar x, const GrB_Vector u,
+                                             const GrB_Descriptor desc);
+GrB_Info GrB_Vector_apply_BinaryOp2nd_Scalar(GrB_Vector w, const GrB_Vector mask,
+                                             const GrB_BinaryOp accum, const GrB_BinaryOp op,
+                                             const GrB_Vector u, const GrB_Scalar y,
+                                             const GrB_Descriptor desc);
+GrB_Info GrB_Matrix_apply_BinaryOp1st_Scalar(GrB_Matrix C, const GrB_Matrix Mask,
+                                             const GrB_BinaryOp accum, const GrB_BinaryOp op,
+                                             const GrB_Scalar x, const GrB_Matrix A,
+                                             const GrB_Descriptor desc);
+GrB_Info GrB_Matrix_apply_BinaryOp2nd_Scalar(GrB_Matrix C, const GrB_Matrix Mask,
+                                             const GrB_BinaryOp accum, const GrB_BinaryOp op,
+                                             const GrB_Matrix A, const GrB_Scalar y,
+                                             const GrB_Descriptor desc);
+
 /* ---------------------------------------------------------------- the hot path */
 /* C<Mask> = C accum (A' (+).(x) B')      replaces SuiteSparse GrB_mxm */
 GrB_Info GrB_mxm(GrB_Matrix C, const GrB_Matrix Mask, const GrB_BinaryOp accum,

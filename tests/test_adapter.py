@@ -39,7 +39,14 @@ names = set(vars(lib))
 for f in ["GrB_mxm", "GrB_mxv", "GrB_vxm", "GrB_Matrix_new", "GrB_Vector_assign_INT32",
           "GrB_Matrix_build_FP64", "GrB_Vector_extractTuples_BOOL", "GrB_Matrix_eWiseMult_BinaryOp",
           "GrB_Vector_reduce_Monoid_Scalar", "GrB_Descriptor_new", "GrB_Matrix_error",
-          "GrB_Matrix_extract", "GrB_Col_extract", "GrB_Vector_extract"]:
+          "GrB_Matrix_extract", "GrB_Col_extract", "GrB_Vector_extract",
+          # GrB_Scalar-argument variants (reference core/vector.py:1406,1449,1769,1808,1918,1939;
+          # core/matrix.py:2392,2435,2837,2902,3279,3305)
+          "GrB_Vector_extractElement_Scalar", "GrB_Matrix_extractElement_Scalar",
+          "GrB_Vector_setElement_Scalar", "GrB_Matrix_setElement_Scalar",
+          "GrB_Vector_assign_Scalar", "GrB_Matrix_assign_Scalar",
+          "GrB_Vector_apply_BinaryOp1st_Scalar", "GrB_Vector_apply_BinaryOp2nd_Scalar",
+          "GrB_Matrix_apply_BinaryOp1st_Scalar", "GrB_Matrix_apply_BinaryOp2nd_Scalar"]:
     assert callable(getattr(lib, f)), f
 assert lib.GrB_SUCCESS == 0 and lib.GrB_NO_VALUE == 1
 sr = [n for n in names if re.match(r"GrB_(PLUS|MIN|MAX)_(PLUS|TIMES|MIN|MAX|FIRST|SECOND)_SEMIRING_", n)]

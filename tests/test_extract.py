@@ -176,3 +176,20 @@ def test_vector_index_assign_replaces_region(gb):
     exp[1] += -1
     exp[5] += -3
     assert dict(zip(i.tolist(), x.tolist())) == exp
+    # the mask aliases the output: the mask is w as it was before the call (the region clear must
+    # not remove the selected positions from it before u is written back)
+    keep = [k for k in range(n) if k != 5]
+    w4 = gb.Vector.from_coo(keep, np.array(keep) + 100, dtype="INT64", size=n)
+    w4(w4.S)[[1, 3, 5, 7]] = u  # selected: 1 (<- -1), 3, 7 (deleted); 5 is outside the mask
+    i, x = w4.to_coo()
+    exp = {k: k + 100 for k in keep if k not in (3, 7)}
+    exp[1] = -1
+    assert dict(zip(i.tolist(), x.tolist())) == exp
+    vals = np.arange(n) + 100
+    vals[1] = 0
+    w5 = gb.Vector.from_coo(np.arange(n), vals, dtype="INT64", size=n)
+    w5(w5.V)[[1, 3, 5, 7]] = u  # value mask: 1 holds 0, so it is not selected and keeps its 0
+    i, x = w5.to_coo()
+    exp = {k: int(vals[k]) for k in range(n) if k not in (3, 7)}
+    exp[5] = -3
+    assert dict(zip(i.tolist(), x.tolist())) == exp
