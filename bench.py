@@ -57,7 +57,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-secondary", action="store_true", help="skip the config 2 / config 4 lines")
     p.add_argument("--no-msbfs", action="store_true", help="skip the multi-source (masked mxm) BFS line")
-    p.add_argument("--msbfs-sharded", action="store_true", help="N > 1: add the row-sharded multi-source BFS line")
+    p.add_argument("--no-msbfs-sharded", action="store_true",
+                   help="N > 1: skip the row-sharded 64-root BFS line (one exchange per level for 64 roots)")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
     # rehearsal of the N>1 path on one GPU: all ranks on one device, gloo transport
@@ -75,7 +76,11 @@ def parse():
     p.add_argument("--spgemm-warmup", type=int, default=1)
     p.add_argument("--no-spgemm", action="store_true", help="skip the config 5 line")
     p.add_argument("--spgemm-scale-big", type=int, default=20,
-                   help="N = 1: a second config 5 line at this scale (the largest that fits one GPU); 0 skips")
+                   help="a second config 5 line at this scale (the largest that fits one GPU); 0 skips")
+    p.add_argument("--spgemm-extra", default="21:2,22:4",
+                   help="more config 5 lines, scale:min_gpus comma-separated (BASELINE.md:35: s21/s22)")
+    p.add_argument("--spgemm-partition", default="products", choices=["products", "equal"],
+                   help="N > 1 config 5: row ranges balanced by Gustavson products, or equal word slots")
     return p.parse_args()
 
 
@@ -266,7 +271,8 @@ def config3_msbfs_sharded(lib, torch, stream, O, args, dist, world, rank, AT, pa
         Vloc<Qloc.V> = d;  Qloc<!Vloc.S, replace> = Q lor.land (A^T shard)^T   (GrB_DESC_RSCT1)
     then the slices' column words (8 B per vertex: all 64 roots' bits) are all-gathered
     straight into Q's words (GxB_Matrix_colwords_view / _touch) -- one collective per level
-    for all 64 roots.  Opt-in (--msbfs-sharded)."""
+    for all 64 roots.  On by default at N > 1 (--no-msbfs-sharded skips it): it is the form of the
+    headline workload whose exchange amortises over 64 roots."""
     from graphblas_amd import device as gdev
     from graphblas_amd import dist as gdist
 
@@ -284,9 +290,13 @@ def config3_msbfs_sharded(lib, torch, stream, O, args, dist, world, rank, AT, pa
     ok(lib.GrB_Matrix_new(ctypes.byref(Ql), lib.GrB_BOOL, K, nloc), "Qloc")
     ok(lib.GrB_Matrix_new(ctypes.byref(Vl), lib.GrB_INT32, K, nloc), "Vloc")
     qi = np.arange(K, dtype=np.uint64)
-    vslot = part["slot"] * 64  # vertices per rank slot (words exchanged per rank)
-    ex = gdist.BitmapAllGather(dist, {"slot": vslot}, world, "cuda")
-    zero_copy = vslot * world == n and args.dist_backend == "nccl"
+    vslot = part["slot"] * 64  # vertices per rank slot (column words exchanged per rank)
+    # the ranks' vertex ranges in column-word units (one word per vertex): with unequal (balanced)
+    # ranges the gather packs them into place (BitmapAllGather's index gather)
+    vb = None if part.get("bounds") is None else [min(n, b * 64) for b in part["bounds"]]
+    ex = gdist.BitmapAllGather(dist, {"slot": vslot, "bounds": vb}, world, "cuda")
+    packed = ex._pack is not None
+    zero_copy = packed or (vslot * world == n and args.dist_backend == "nccl")
     nv = ctypes.c_uint64()
     sr, desc, ALL = _bfs_semiring(lib, args), lib.GrB_DESC_RSCT1, lib.GrB_ALL
 
@@ -343,7 +353,9 @@ def config3_msbfs_sharded(lib, torch, stream, O, args, dist, world, rank, AT, pa
     dist.all_gather(allv, row0.to(dev))
     parity = None
     if rank == 0:
-        got = torch.cat([t.cpu() for t in allv]).numpy()[:n]
+        # rank k's slice belongs at its range [lo_k, hi_k)
+        b = vb if vb is not None else [min(n, k * vslot) for k in range(world + 1)]
+        got = np.concatenate([allv[k].cpu().numpy()[:b[k + 1] - b[k]] for k in range(world)])
         lev, _, _ = O.bfs_levels(O.rmat(args.scale, args.edge_factor, args.seed), int(roots[0]))
         parity = bool(np.array_equal(got, lev))
     for _ in range(2):
@@ -536,25 +548,53 @@ def config4_masked_spgemm(lib, torch, stream, O, args, s4, cpu=False):
     return res
 
 
-def config5_spgemm(lib, torch, stream, dist, world, rank, args):
-    """SURVEY 8(d) config 5 / 8(e) mxm row: C = A plus.times A, FP64, unmasked, on R-MAT
-    (scale args.spgemm_scale; s23 does not fit 8 x 288 GB), 1-D row shards.
-    Rank r holds rows [lo, hi) of A (generated as a row shard), which is also its panel of B;
-    one step = the all-gatherv of B's CSR row panels over RCCL (dist.RowPanelAllGather, on the
-    library stream) + GxB_Matrix_import_device + the local GrB_mxm(C_r, A_r, B).  Total work is
-    fixed as N grows.  GTEPS = products (sum over A's entries (i,k) of |B(k,:)|) / max-over-ranks
-    time.  Parity: 16 sampled rows of each rank's C_r against a numpy fold of the same rows
-    (fp64, rtol 1e-6; structure exact)."""
+def config5_spgemm(lib, torch, stream, O, dist, world, rank, args, sc, cpu=False):
+    """SURVEY 8(d) config 5 / 8(e) mxm row: C = A plus.times A, FP64, unmasked, on R-MAT scale sc
+    (s23 does not fit 8 x 288 GB; BASELINE.md:35 asks for s21/s22), 1-D row shards.
+    Rank r holds rows [lo, hi) of A (generated as a row shard), which is also its panel of B; with
+    N > 1 the row ranges are balanced by Gustavson products (dist.product_balanced_bounds: SpGEMM
+    work on R-MAT is far more skewed than entry counts).  One step = the all-gatherv of B's CSR row
+    panels over RCCL (dist.RowPanelAllGather, on the library stream) + GxB_Matrix_import_device +
+    the local GrB_mxm(C_r, A_r, B).  Total work is fixed as N grows (strong scaling).
+    GTEPS = products (sum over A's entries (i,k) of |B(k,:)|) / max-over-ranks time.
+    Parity: 16 sampled rows of each rank's C_r (its longest rows first) against a numpy fold of the
+    same rows (fp64, rtol 1e-6; structure exact).
+    roofline: SURVEY 8(d)'s compulsory bytes per GPU (A_r and B read once, C_r written once, the
+    panels received) / the step time; `stream` beside it prices Gustavson's B-row reads (12 B per
+    product) instead of one read of B.  traffic: HBM bytes per call from the committed PMC table
+    (N = 1).  cpu_baseline (cpu=True, N = 1): oracle or_spgemm_plus_times_fp64_par (OpenMP
+    Gustavson, all host threads) on the leading rows (labels are scrambled: a random sample),
+    its rows checked against the GPU's."""
     from graphblas_amd import device as gdev
     from graphblas_amd import dist as gdist
 
-    sc = args.spgemm_scale
     n = 1 << sc
+    xdev = "cuda" if args.dist_backend == "nccl" else "cpu"
     part = gdist.partition(n, world, rank)
     lo, hi = part["lo"], part["hi"]
     A = ctypes.c_void_p()
     ok(lib.GxB_Matrix_rmat(ctypes.byref(A), sc, args.edge_factor, args.seed, 2, 2, lo, hi), "rmat fp64 row panel")
     torch.cuda.synchronize()
+    balance = None
+    if world > 1 and args.spgemm_partition == "products":
+        va = gdev.matrix_view(A)
+        rp = gdev.device_tensor(torch, va.rowptr, va.nrows + 1)
+        ci = gdev.device_tensor(torch, va.colidx, va.nvals, "<i4")
+        bounds, wp = gdist.product_balanced_bounds(dist, torch, n, world, rank, rp, ci, xdev)
+        del rp, ci
+        eq = [gdist.partition(n, world, k) for k in range(world)]
+        cw = np.concatenate([[0], np.cumsum(wp)])
+        part = gdist.partition(n, world, rank, bounds)
+        balance = {"partition": "rows balanced by products",
+                   "products_per_rank_equal_slots": [int(cw[p["hi_w"]] - cw[p["lo_w"]]) for p in eq],
+                   "products_per_rank": [int(cw[bounds[k + 1]] - cw[bounds[k]]) for k in range(world)]}
+        if (part["lo"], part["hi"]) != (lo, hi):
+            lo, hi = part["lo"], part["hi"]
+            ok(lib.GrB_Matrix_free(ctypes.byref(A)), "free shard")
+            A = ctypes.c_void_p()
+            ok(lib.GxB_Matrix_rmat(ctypes.byref(A), sc, args.edge_factor, args.seed, 2, 2, lo, hi),
+               "rmat fp64 balanced row panel")
+            torch.cuda.synchronize()
     va = gdev.matrix_view(A)
     nr, nnz_a = va.nrows, va.nvals
     gath = gdist.RowPanelAllGather(dist, world, rank) if world > 1 else None
@@ -562,37 +602,61 @@ def config5_spgemm(lib, torch, stream, dist, world, rank, args):
     nv = ctypes.c_uint64()
     keep = {}
 
+    def gather():
+        with torch.cuda.stream(stream):
+            B, _ = gdist.gather_row_panels(lib, torch, gath, A, n)
+        return B
+
     def step(keep_c=False):
-        if world > 1:
-            with torch.cuda.stream(stream):
-                B, brp = gdist.gather_row_panels(lib, torch, gath, A, n)
-        else:
-            B = A
+        B = gather() if world > 1 else A
         C = ctypes.c_void_p()
         ok(lib.GrB_Matrix_new(ctypes.byref(C), lib.GrB_FP64, nr, n), "C")
-        ok(lib.GrB_mxm(C, None, None, sr, A, B, None), "mxm")
-        ok(lib.GrB_Matrix_nvals(ctypes.byref(nv), C), "nvals C")
-        if keep_c:
+        rc = lib.GrB_mxm(C, None, None, sr, A, B, None)
+        if rc == 0:
+            ok(lib.GrB_Matrix_nvals(ctypes.byref(nv), C), "nvals C")
+        if keep_c and rc == 0:
             keep["C"], keep["B"] = C, B
         else:
             ok(lib.GrB_Matrix_free(ctypes.byref(C)), "free C")
             if world > 1:
                 ok(lib.GrB_Matrix_free(ctypes.byref(B)), "free B")
+        if rc != 0:
+            return -rc  # GrB_Info codes are negative
         return nv.value
 
+    def agree(flag):
+        """every rank's flag, max-reduced (a failed rank makes all ranks skip together)"""
+        if not dist:
+            return flag
+        t = torch.tensor([flag], dtype=torch.int64, device=xdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return int(t.item())
+
     # untimed: one step kept for the product count and the parity sample
-    nnz_c = step(keep_c=True)
+    r0 = step(keep_c=True)
+    failed = agree(1 if "C" not in keep else 0)
+    if failed:
+        ok(lib.GrB_Matrix_free(ctypes.byref(A)), "free A")
+        for h in ("C", "B"):
+            if h in keep:
+                lib.GrB_Matrix_free(ctypes.byref(keep[h]))
+        return {"workload": f"C = A plus.times A, R-MAT s{sc}, 1-D row shards x{world}",
+                "skipped": f"GrB_mxm failed on at least one rank (this rank's GrB_Info: "
+                           f"{-r0 if 'C' not in keep else 0}; -102 = out of device memory)"}
+    nnz_c = r0
     B = keep["B"]
     vb = gdev.matrix_view(B)
     brp = gdev.device_tensor(torch, vb.rowptr, n + 1)
     deg = brp[1:] - brp[:-1]
     aci = gdev.device_tensor(torch, va.colidx, nnz_a, "<i4").long()
-    prods = int(deg[aci].sum().item())
+    arp_t = gdev.device_tensor(torch, va.rowptr, nr + 1)
+    rprod = gdist.row_products(torch, arp_t, aci, deg)
+    prods = int(rprod.sum().item())
     # parity sample (host): rows of C_r vs a numpy fold over A_r and B
     C = keep["C"]
     vc = gdev.matrix_view(C)
     crp = gdev.device_tensor(torch, vc.rowptr, nr + 1).cpu().numpy()
-    arp = gdev.device_tensor(torch, va.rowptr, nr + 1).cpu().numpy()
+    arp = arp_t.cpu().numpy()
     ax = gdev.device_tensor(torch, va.values, nnz_a, "<f8").cpu().numpy()
     ai = aci.cpu().numpy()
     bp = brp.cpu().numpy()
@@ -600,7 +664,11 @@ def config5_spgemm(lib, torch, stream, dist, world, rank, args):
     bx = gdev.device_tensor(torch, vb.values, vb.nvals, "<f8").cpu().numpy()
     cit = gdev.device_tensor(torch, vc.colidx, vc.nvals, "<i4")
     cvt = gdev.device_tensor(torch, vc.values, vc.nvals, "<f8")
-    rows = np.sort(np.random.default_rng(11 + rank).choice(nr, min(16, nr), replace=False)) if nr else []
+    rows = []
+    if nr:
+        heavy = torch.argsort(rprod, descending=True)[:3].cpu().numpy()  # the column-window bins
+        rnd = np.random.default_rng(11 + rank).choice(nr, min(12, nr), replace=False)
+        rows = np.unique(np.concatenate([heavy, rnd]))
     parity = True
     for r in rows:
         acc = np.zeros(n)
@@ -614,9 +682,52 @@ def config5_spgemm(lib, torch, stream, dist, world, rank, args):
         gc = cit[crp[r]:crp[r + 1]].cpu().numpy()
         gv = cvt[crp[r]:crp[r + 1]].cpu().numpy()
         parity &= bool(np.array_equal(gc, cols) and np.allclose(gv, acc[cols], rtol=1e-6, atol=0))
+    cpu_res = None
+    if cpu and world == 1 and not args.no_cpu_baseline:
+        # the same product on all host threads over the leading rows [0, r1), doubling r1 until the
+        # sample takes about --cpu-secondary-seconds / 2 or its C would pass 1.5e8 entries (host
+        # memory of the check); checked against the GPU's rows
+        th = _threads()
+        Ah = O.Csr(n, n, "FP64", arp, ai, ax)
+        r1 = max(64, n >> 12)
+        cap = 150_000_000
+        while True:
+            t1 = time.perf_counter()
+            Cc, prods_c = O.spgemm_plus_times_fp64_par(Ah, Ah, 0, r1, th)
+            tc = time.perf_counter() - t1
+            if tc >= args.cpu_secondary_seconds / 2 or r1 >= n or int(crp[min(n, 2 * r1)]) > cap:
+                break
+            r1 = min(n, r1 * 2)
+        e1 = int(crp[r1])
+        gci = cit[:e1].cpu().numpy().astype(np.int64)
+        gcv = cvt[:e1].cpu().numpy()
+        cpu_ok = bool(np.array_equal(Cc.indptr, crp[:r1 + 1]) and np.array_equal(Cc.indices, gci) and
+                      np.allclose(Cc.values, gcv, rtol=1e-6, atol=0))
+        cpu_res = {"value": prods_c / tc / 1e9, "unit": "GTEPS", "cores": th, "kind": "port", "matches_gpu": cpu_ok,
+                   "gteps_def": "products per second (the GPU line's definition)",
+                   "sample": f"rows [0, {r1}) of {n} ({prods_c:.3e} products, {Cc.nvals} entries of C), {tc:.1f} s "
+                             f"on {th} host threads: Gustavson with a dense per-thread accumulator (oracle "
+                             f"or_spgemm_plus_times_fp64_par, OpenMP; not SuiteSparse)"}
+        del Ah, Cc
+    del cit, cvt, aci, arp_t, rprod, brp, deg
     ok(lib.GrB_Matrix_free(ctypes.byref(C)), "free C")
     if world > 1:
         ok(lib.GrB_Matrix_free(ctypes.byref(B)), "free B")
+    # the exchange alone (untimed pass): panel all-gather + import, bytes received per rank
+    xg = None
+    if world > 1:
+        torch.cuda.synchronize()
+        dist.barrier()
+        t1 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            Bx = gather()
+            torch.cuda.synchronize()
+            ok(lib.GrB_Matrix_free(ctypes.byref(Bx)), "free B")
+        tx = (time.perf_counter() - t1) / reps
+        t = torch.tensor([tx], dtype=torch.float64, device=xdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tx = float(t.item())
     for _ in range(args.spgemm_warmup):
         step()
     torch.cuda.synchronize()
@@ -631,29 +742,46 @@ def config5_spgemm(lib, torch, stream, dist, world, rank, args):
         dist.barrier()
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / args.spgemm_steps
-    tot = [prods, nnz_c, nnz_a, int(parity)]
+    # per-rank compulsory bytes: A_r read, B read, C_r written (+ the other ranks' panels received)
+    panel_rx = (12 * (vb.nvals - nnz_a) + 8 * (n - nr)) if world > 1 else 0
+    by_r = (12 * nnz_a + 8 * (nr + 1)) + (12 * vb.nvals + 8 * (n + 1)) + (12 * nnz_c + 8 * (nr + 1)) + panel_rx
+    st_r = (12 * nnz_a + 8 * (nr + 1)) + 12 * prods + (12 * nnz_c + 8 * (nr + 1)) + panel_rx
+    tot = [prods, nnz_c, nnz_a, 1 - int(parity), by_r, st_r, panel_rx]
     if dist:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        t = torch.tensor([el], dtype=torch.float64, device=xdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-        tt = torch.tensor(tot[:3] + [1 - tot[3]], dtype=torch.int64, device="cuda")
+        tt = torch.tensor(tot, dtype=torch.int64, device=xdev)
         dist.all_reduce(tt)
         tot = [int(x) for x in tt.tolist()]
-        tot[3] = int(tot[3] == 0)
-    prods_all, nnzc_all, nnza_all, par_all = tot
-    # bytes per step: A and B as CSR read, C written, the panels' exchange
-    by = 2 * (12 * nnza_all + 8 * (n + 1)) + 12 * nnzc_all + 8 * (n + 1)
-    if world > 1:
-        by += world * (12 * nnza_all + 8 * n)  # every rank receives the whole B
+    prods_all, nnzc_all, nnza_all, nfail, by_all, st_all, rx_all = tot
     ok(lib.GrB_Matrix_free(ctypes.byref(A)), "free A")
-    return {
+    traffic, src = _profile_traffic(f"r04_config5_s{sc}_pmc.json") if world == 1 else (None, None)
+    roof = _roofline(by_all / world, el, traffic, src, "one GrB_mxm call per GPU (k_row_flops, hash bins, "
+                                                       "k_row_window, k_window_num, segmented sort)")
+    roof["alg_bytes_def"] = ("SURVEY 8(d) config 5, per GPU: 12 nnz(A_r) + 12 nnz(B) + 12 nnz(C_r) + row pointers "
+                             "+ the panels received")
+    res = {
         "workload": f"C = A plus.times A (GrB_mxm, unmasked, FP64 U[0,1)), R-MAT s{sc} ef {args.edge_factor}, "
                     f"1-D row shards x{world}, B row panels all-gathered over "
                     f"{'RCCL' if world > 1 else '(none: one GPU)'}",
         "n": n, "nnz_A": nnza_all, "nnz_C": nnzc_all, "products": prods_all, "ms": el * 1e3,
         "gteps": prods_all / el / 1e9, "gteps_def": "products (sum over A(i,k) of |B(k,:)|) per second",
-        "alg_bytes": by, "hbm_GBs_per_gpu": by / world / el / 1e9, "parity_sampled_rows": bool(par_all),
+        "alg_bytes": by_all, "hbm_GBs_per_gpu": by_all / world / el / 1e9, "parity_sampled_rows": nfail == 0,
+        "roofline": roof,
+        "roofline_stream": _roofline(st_all / world, el, None, None, "the same call, B rows priced per product "
+                                                                    "(12 B each): Gustavson's streamed bytes"),
         "steps": args.spgemm_steps, "warmup": args.spgemm_warmup, "scaling": "strong"}
+    if balance:
+        res["balance"] = balance
+    if world > 1:
+        res["allgather"] = {"bytes_received_per_rank_avg": rx_all / world, "ms": tx * 1e3,
+                            "GBs_per_rank": rx_all / world / tx / 1e9,
+                            "what": "B's row panels all-gathered (RowPanelAllGather: sizes, then one "
+                                    "all_gather_into_tensor) + GxB_Matrix_import_device, max over ranks"}
+    if cpu_res:
+        res["cpu_baseline"] = cpu_res
+    return res
 
 
 def main():
@@ -956,7 +1084,7 @@ def main():
                     f"({'GrB_LOR_LAND_SEMIRING_BOOL' if other == 'lor_land' else 'GxB_ANY_PAIR_BOOL'}), "
                     f"the {len(roots)} roots once each", "gteps": sum(edges) / el_o / 1e9,
         "ms_per_bfs": el_o / len(roots) * 1e3, "parity_vs_oracle_root0": par_other}
-    if world > 1 and args.msbfs_sharded:
+    if world > 1 and not args.no_msbfs_sharded:
         secondary["config3_msbfs_64_roots_sharded"] = config3_msbfs_sharded(
             lib, torch, stream, O, args, dist, world, rank, A, part, deg, roots)
     if rank == 0 and world == 1 and not args.no_msbfs:
@@ -964,13 +1092,21 @@ def main():
     if rank == 0 and world == 1 and not args.no_secondary:
         secondary.update(secondary_workloads(lib, torch, stream, O, args))
     if not args.no_spgemm:
-        secondary["config5_spgemm_plus_times_fp64"] = config5_spgemm(lib, torch, stream, dist, world, rank, args)
-        if world == 1 and args.spgemm_scale_big > args.spgemm_scale:
-            # the largest unmasked scale that fits one GPU (s20: C has 9.7e9 entries, 116 GB)
-            big = argparse.Namespace(**vars(args))
-            big.spgemm_scale = args.spgemm_scale_big
-            secondary[f"config5_spgemm_plus_times_fp64_s{big.spgemm_scale}"] = config5_spgemm(
-                lib, torch, stream, dist, world, rank, big)
+        # config 5 lines: s19 (every N), s20 (every N: pairs the N = 1 line, the largest scale one GPU
+        # holds), and from --spgemm-extra the scales BASELINE.md:35 names for larger N (s21 at N >= 2,
+        # s22 at N >= 4); a scale whose C does not fit is reported as skipped, not failed
+        scales = [(args.spgemm_scale, 1)]
+        if args.spgemm_scale_big > args.spgemm_scale:
+            scales.append((args.spgemm_scale_big, 1))
+        for kv in [x for x in args.spgemm_extra.split(",") if x]:
+            s_, w_ = (int(v) for v in kv.split(":"))
+            scales.append((s_, w_))
+        for s5, wmin in scales:
+            if world < wmin:
+                continue
+            key = "config5_spgemm_plus_times_fp64" + ("" if s5 == args.spgemm_scale else f"_s{s5}")
+            secondary[key] = config5_spgemm(lib, torch, stream, O, dist, world, rank, args, s5,
+                                            cpu=s5 == args.spgemm_scale)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -60,9 +60,11 @@ GB_HD D gb_cast(S x) {
     } else if constexpr (std::is_same<S, bool>::value) {
         return (D)(x ? 1 : 0);
     } else if constexpr (std::is_integral<S>::value && std::is_integral<D>::value) {
-        // two's complement wrap (modular)
+        // C's integer conversion: the value modulo 2^bits(D) (signed sources sign-extend when
+        // widening -- converting to S's unsigned type first would zero-extend: int32 -5 -> int64
+        // 4294967291)
         using UD = typename std::make_unsigned<D>::type;
-        return (D)(UD)(typename std::make_unsigned<S>::type)x;
+        return (D)(UD)x;
     } else {
         return (D)x;
     }

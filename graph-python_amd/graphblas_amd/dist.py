@@ -44,6 +44,63 @@ def balanced_bounds(word_nnz, world):
     return b
 
 
+def gather_slots(dist, torch, world, local, slot, counts, device):
+    """Concatenation in rank order of every rank's 1-D int64 `local` (rank k contributes its
+    first counts[k] entries): padded to `slot`, one all-gather, unpadded on the host -> numpy."""
+    send = torch.zeros(slot, dtype=torch.int64, device=device)
+    send[:local.numel()] = local.to(device)
+    got = torch.zeros(slot * world, dtype=torch.int64, device=device)
+    dist.all_gather(list(got.chunk(world)), send)
+    g = got.cpu().numpy()
+    return np.concatenate([g[k * slot:k * slot + counts[k]] for k in range(world)])
+
+
+def gather_word_weights(dist, torch, n, world, word_w, device):
+    """All ranks' per-64-row-word weights in word order (numpy int64[words]), from each rank's
+    weights for the words of its equal slot (partition(n, world, rank) without bounds)."""
+    ps = [partition(n, world, k) for k in range(world)]
+    return gather_slots(dist, torch, world, word_w, ps[0]["slot"], [p["hi_w"] - p["lo_w"] for p in ps], device)
+
+
+def gather_row_weights(dist, torch, n, world, row_w, device):
+    """All ranks' per-row weights in row order (numpy int64[n]), from each rank's weights for
+    the rows of its equal slot (e.g. the row lengths of its row shard: B's degrees)."""
+    ps = [partition(n, world, k) for k in range(world)]
+    return gather_slots(dist, torch, world, row_w, ps[0]["slot"] * 64, [p["hi"] - p["lo"] for p in ps], device)
+
+
+def product_balanced_bounds(dist, torch, n, world, rank, rowptr, colidx, device):
+    """1-D row ranges of C = A * A balanced by Gustavson products (the work of row i is
+    sum over A(i, k) of |A(k,:)|; SpGEMM work on R-MAT is far more skewed than entry counts):
+    every rank holds the row shard of its equal slot (rowptr / colidx, local rows); the shards'
+    row lengths are all-gathered into the global degrees, each rank sums its rows' products
+    per 64-row word, the word sums are all-gathered and cut into equal-product ranges.
+    Returns (bounds, word_products)."""
+    deg_loc = (rowptr[1:] - rowptr[:-1]).to(torch.int64)
+    deg = torch.from_numpy(gather_row_weights(dist, torch, n, world, deg_loc, device)).to(rowptr.device)
+    rp = row_products(torch, rowptr, colidx, deg)
+    p = partition(n, world, rank)
+    wp = gather_word_weights(dist, torch, n, world, word_sums(torch, rp, p["hi_w"] - p["lo_w"]), device)
+    return balanced_bounds(wp, world), wp
+
+
+def row_products(torch, rowptr, colidx, deg):
+    """Gustavson work per row of a row panel A_r of C_r = A_r * B: sum over A_r(i, k) of |B(k,:)|
+    (deg = B's row lengths, indexed by A's column ids).  rowptr int64[nr + 1] (from 0), colidx
+    int32/int64[nnz]; torch tensors on any device -> int64[nr]."""
+    f = deg[colidx.long()].to(torch.int64)
+    cs = torch.zeros(f.numel() + 1, dtype=torch.int64, device=f.device)
+    torch.cumsum(f, 0, out=cs[1:])
+    return cs[rowptr[1:]] - cs[rowptr[:-1]]
+
+
+def word_sums(torch, row_w, nwords):
+    """Per-64-row-word sums of a per-row weight vector (zero-padded to nwords * 64 rows)."""
+    pad = torch.zeros(nwords * 64, dtype=torch.int64, device=row_w.device)
+    pad[:row_w.numel()] = row_w
+    return pad.view(nwords, 64).sum(1)
+
+
 class BitmapAllGather:
     """All-gather of int64 bitmap slices into one frontier bitmap.
 

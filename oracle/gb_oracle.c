@@ -880,3 +880,86 @@ int64_t or_masked_dot_min_plus_int64_par(const or_csr *A, const or_csr *AT, int6
     if (work) *work = wk;
     return nc;
 }
+
+static int cmp_i64_asc(const void *a, const void *b) {
+    const int64_t x = *(const int64_t *)a, y = *(const int64_t *)b;
+    return (x > y) - (x < y);
+}
+
+/* C = A plus.times B (FP64, unmasked) over the rows [row0, row1) of A: Gustavson's row-wise
+ * saxpy with a dense accumulator per thread (values + a row stamp + the list of touched
+ * columns, sorted when the row is done) -- the method a CPU GraphBLAS library uses for an
+ * unmasked A*B (SuiteSparse saxpy3's Gustavson variant), nthreads host threads, rows handed
+ * out dynamically.  Each output value folds its products in ascending k (A's row order), like
+ * or_mxm.  C (rows row1 - row0, B->ncols columns) is allocated here; *products = sum over the
+ * rows' entries A(i,k) of |B(k,:)|.  Returns nnz(C). */
+int64_t or_spgemm_plus_times_fp64_par(const or_csr *A, const or_csr *B, int64_t row0, int64_t row1, or_csr *C,
+                                      int64_t *products, int nthreads) {
+    const int64_t nr = row1 - row0, n = B->ncols;
+    const double *ax = (const double *)A->x, *bx = (const double *)B->x;
+    if (nthreads < 1) nthreads = 1;
+    int64_t *rlen = (int64_t *)calloc((size_t)nr + 1, sizeof(int64_t));
+    int64_t **rcol = (int64_t **)calloc((size_t)nr + 1, sizeof(int64_t *));
+    double **rval = (double **)calloc((size_t)nr + 1, sizeof(double *));
+    int64_t prods = 0;
+#pragma omp parallel num_threads(nthreads) reduction(+ : prods)
+    {
+        double *acc = (double *)malloc((size_t)n * sizeof(double));
+        int64_t *stamp = (int64_t *)malloc((size_t)n * sizeof(int64_t));
+        int64_t *cols = (int64_t *)malloc((size_t)n * sizeof(int64_t));
+        for (int64_t c = 0; c < n; c++) stamp[c] = -1;
+#pragma omp for schedule(dynamic, 16)
+        for (int64_t i = row0; i < row1; i++) {
+            int64_t m = 0;
+            for (int64_t e = A->p[i]; e < A->p[i + 1]; e++) {
+                const int64_t k = A->j[e];
+                const double a = ax[e];
+                prods += B->p[k + 1] - B->p[k];
+                for (int64_t q = B->p[k]; q < B->p[k + 1]; q++) {
+                    const int64_t c = B->j[q];
+                    if (stamp[c] != i) {
+                        stamp[c] = i;
+                        acc[c] = a * bx[q];
+                        cols[m++] = c;
+                    } else {
+                        acc[c] += a * bx[q];
+                    }
+                }
+            }
+            qsort(cols, (size_t)m, sizeof(int64_t), cmp_i64_asc);
+            int64_t *rc = (int64_t *)xmalloc((size_t)m * sizeof(int64_t));
+            double *rv = (double *)xmalloc((size_t)m * sizeof(double));
+            for (int64_t t = 0; t < m; t++) {
+                rc[t] = cols[t];
+                rv[t] = acc[cols[t]];
+            }
+            rlen[i - row0] = m;
+            rcol[i - row0] = rc;
+            rval[i - row0] = rv;
+        }
+        free(acc);
+        free(stamp);
+        free(cols);
+    }
+    C->nrows = nr;
+    C->ncols = n;
+    C->type = GBAMD_T_FP64;
+    C->p = (int64_t *)xmalloc(((size_t)nr + 1) * sizeof(int64_t));
+    C->p[0] = 0;
+    for (int64_t r = 0; r < nr; r++) C->p[r + 1] = C->p[r] + rlen[r];
+    const int64_t nz = C->p[nr];
+    C->j = (int64_t *)xmalloc((size_t)nz * sizeof(int64_t));
+    C->x = xmalloc((size_t)nz * sizeof(double));
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 64)
+    for (int64_t r = 0; r < nr; r++) {
+        memcpy(C->j + C->p[r], rcol[r], (size_t)rlen[r] * sizeof(int64_t));
+        memcpy((double *)C->x + C->p[r], rval[r], (size_t)rlen[r] * sizeof(double));
+        free(rcol[r]);
+        free(rval[r]);
+    }
+    free(rlen);
+    free(rcol);
+    free(rval);
+    if (products) *products = prods;
+    return nz;
+}

@@ -314,6 +314,20 @@ def masked_dot_min_plus_int64_par(A, AT, row0, row1, nthreads):
     return vals[:m], present[:m].astype(bool), int(nc), work.value
 
 
+def spgemm_plus_times_fp64_par(A, B, row0, row1, nthreads):
+    """CPU baseline (config 5): C = A plus.times B (FP64 Csr, unmasked) over the rows [row0, row1)
+    of A, Gustavson on nthreads host threads; -> (C rows as a Csr, products)."""
+    out = _Csr()
+    prods = ctypes.c_int64(0)
+    f = lib().or_spgemm_plus_times_fp64_par
+    f.restype = ctypes.c_int64
+    f(ctypes.byref(A._c()), ctypes.byref(B._c()), ctypes.c_int64(row0), ctypes.c_int64(row1), ctypes.byref(out),
+      ctypes.byref(prods), ctypes.c_int(nthreads))
+    C = Csr._from_c(out, "FP64")
+    lib().or_csr_free(ctypes.byref(out))
+    return C, prods.value
+
+
 def bfs_graphblas(A, src):
     """The Level-BFS loop of the reference notebook (Example B.1 cell 8) through or_mxm:
        v[:](mask=q.V) << d ; q(~v.S, replace) << q.vxm(A, lor_land) ; stop when q empty."""

@@ -71,3 +71,18 @@ def test_spmv_cpu_baseline_matches_scipy():
     S = sp.csr_matrix((A.values, A.indices, A.indptr), shape=(A.nrows, A.ncols))
     assert np.array_equal(present, np.diff(AT.indptr) > 0)
     assert np.allclose(y, S.T @ x, rtol=1e-12, atol=0)
+
+
+def test_spgemm_cpu_baseline_matches_oracle():
+    """bench.py config-5 cpu_baseline: or_spgemm_plus_times_fp64_par == or_mxm (same ascending-k
+    fold: bit-identical), on the whole matrix and on a row range"""
+    A = O.rmat(10, 8, 42, values="FP64", value_seed=2)
+    ref = O.mxm(O.Csr.empty(A.nrows, A.ncols, "FP64"), A, A, ("PLUS", "TIMES", "FP64"))
+    deg = np.diff(A.indptr)
+    for r0, r1, nt in ((0, A.nrows, 4), (200, 700, 1), (5, 5, 2)):
+        C, prods = O.spgemm_plus_times_fp64_par(A, A, r0, r1, nt)
+        p0, p1 = ref.indptr[r0], ref.indptr[r1]
+        assert np.array_equal(C.indptr, ref.indptr[r0:r1 + 1] - p0)
+        assert np.array_equal(C.indices, ref.indices[p0:p1])
+        assert np.array_equal(C.values, ref.values[p0:p1])
+        assert prods == int(deg[A.indices[A.indptr[r0]:A.indptr[r1]]].sum())

@@ -159,3 +159,88 @@ def test_row_panel_mixed_iso(kinds):
             assert bvx.size == 1 and bvx[0] == kinds[0][1]
         else:
             assert np.array_equal(bvx, expect)
+
+
+def _degree_sorted_fp64(G):
+    """G relabelled so ids fall with out-degree (hubs first): equal row slots give rank 0 most of
+    the Gustavson work"""
+    order = np.argsort(-np.diff(G.indptr), kind="stable")
+    new = np.empty_like(order)
+    new[order] = np.arange(order.size)
+    rows = new[np.repeat(np.arange(G.nrows), np.diff(G.indptr))]
+    return O.Csr.from_coo(rows, new[G.indices], G.values, nrows=G.nrows, ncols=G.ncols, dtype="FP64")
+
+
+def _balanced_worker(rank, world, port, scale, out_q):
+    """bench.py config 5 at N > 1: equal-slot shards -> product-balanced bounds -> re-cut shards ->
+    panel all-gather -> local product"""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    G = _degree_sorted_fp64(O.rmat(scale, 8, 42, values="FP64", value_seed=2))
+    n = G.nrows
+    eq = gdist.partition(n, world, rank)
+    p0, p1 = int(G.indptr[eq["lo"]]), int(G.indptr[eq["hi"]])
+    rp = torch.from_numpy(G.indptr[eq["lo"]:eq["hi"] + 1] - p0)
+    ci = torch.from_numpy(G.indices[p0:p1].astype(np.int32))
+    bounds, wp = gdist.product_balanced_bounds(dist, torch, n, world, rank, rp, ci, "cpu")
+    part = gdist.partition(n, world, rank, bounds)
+    lo, hi = part["lo"], part["hi"]
+    p0, p1 = int(G.indptr[lo]), int(G.indptr[hi])
+    rp = torch.from_numpy(G.indptr[lo:hi + 1] - p0)
+    ci = torch.from_numpy(G.indices[p0:p1].astype(np.int32))
+    vx = torch.from_numpy(G.values[p0:p1].copy())
+    brp, bci, bvx, _ = gdist.RowPanelAllGather(dist, world, rank).run(rp, ci, vx)
+    B = O.Csr(n, n, "FP64", brp.numpy(), bci.numpy(), bvx.numpy())
+    Ar = O.Csr(hi - lo, n, "FP64", rp.numpy(), ci.numpy(), vx.numpy())
+    C = O.mxm(O.Csr.empty(hi - lo, n, "FP64"), Ar, B, ("PLUS", "TIMES", "FP64"))
+    out_q.put((rank, bounds, wp, lo, hi, C.indptr, C.indices, C.values))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_product_balanced_bounds(world):
+    """dist.product_balanced_bounds (bench.py config 5, N > 1): every rank derives the same row
+    ranges; the per-word products equal a direct count; each range carries at most total/world plus
+    one word's products; on a hubs-first graph it evens out what equal slots leave on rank 0; and the
+    stacked local products over the re-cut ranges are the oracle's C (bit-exact)"""
+    scale = 9
+    G = _degree_sorted_fp64(O.rmat(scale, 8, 42, values="FP64", value_seed=2))
+    n = G.nrows
+    deg = np.diff(G.indptr)
+    row_prod = np.add.reduceat(np.concatenate([deg[G.indices], [0]]), G.indptr[:-1])
+    row_prod[deg == 0] = 0
+    words = (n + 63) // 64
+    wp_ref = np.zeros(words * 64, np.int64)
+    wp_ref[:n] = row_prod
+    wp_ref = wp_ref.reshape(words, 64).sum(1)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_balanced_worker, args=(r, world, port, scale, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    bounds = res[0][1]
+    for r in res:
+        assert r[1] == bounds and np.array_equal(r[2], wp_ref)
+    cw = np.concatenate([[0], np.cumsum(wp_ref)])
+    tot = int(cw[-1])
+    per = [int(cw[bounds[k + 1]] - cw[bounds[k]]) for k in range(world)]
+    assert sum(per) == tot and max(per) <= tot / world + int(wp_ref.max())
+    eq = [int(cw[gdist.partition(n, world, k)["hi_w"]] - cw[gdist.partition(n, world, k)["lo_w"]])
+          for k in range(world)]
+    assert max(per) < max(eq)
+    ref = O.mxm(O.Csr.empty(n, n, "FP64"), G, G, ("PLUS", "TIMES", "FP64"))
+    cp, cidx, cval, base = [np.zeros(1, np.int64)], [], [], 0
+    for _, _, _, lo, hi, rp, idx, val in res:
+        cp.append(rp[1:] + base)
+        base += int(rp[-1])
+        cidx.append(idx)
+        cval.append(val)
+    assert np.array_equal(np.concatenate(cp), ref.indptr)
+    assert np.array_equal(np.concatenate(cidx), ref.indices)
+    assert np.array_equal(np.concatenate(cval), ref.values)

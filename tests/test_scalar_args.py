@@ -222,3 +222,36 @@ def test_apply_binaryop_scalar(gb):
     assert b"no value" in msg.value
     for h in (s, f, e):
         lib.GrB_Scalar_free(ctypes.byref(h))
+
+
+@pytest.mark.parametrize("src,dst", [("INT8", "INT64"), ("INT16", "INT32"), ("INT32", "INT64"), ("INT8", "UINT64"),
+                                     ("INT64", "INT8"), ("UINT32", "INT64"), ("INT32", "UINT16")])
+def test_integer_casts_follow_c(gb, src, dst):
+    """C's integer conversions (SuiteSparse GB_cast for integer types): widening sign-extends a
+    signed source, narrowing keeps the value modulo 2^bits -- numpy's astype gives the same --
+    through a typed setElement, a GrB_Scalar setElement, an assign of a whole vector, and apply"""
+    lib = gb.lib
+    vals = np.array([-5, -1, 0, 7, -128, 127], dtype=np.int64)
+    sv = vals.astype(getattr(np, src.lower()))
+    exp = sv.astype(getattr(np, dst.lower()))
+    n = len(vals)
+    ct = {"INT8": ctypes.c_int8, "INT16": ctypes.c_int16, "INT32": ctypes.c_int32, "INT64": ctypes.c_int64,
+          "UINT32": ctypes.c_uint32}[src]
+    w = gb.Vector(getattr(gb, dst), n)
+    for i, x in enumerate(sv.tolist()):
+        assert getattr(lib, f"GrB_Vector_setElement_{src}")(w._carg, ct(x), i) == 0
+    i, got = w.to_coo()
+    assert np.array_equal(got, exp)
+    w2 = gb.Vector(getattr(gb, dst), n)
+    for k, x in enumerate(sv.tolist()):
+        s = _scalar(lib, src, x)
+        assert lib.GrB_Vector_setElement_Scalar(w2._carg, s, k) == 0
+        lib.GrB_Scalar_free(ctypes.byref(s))
+    assert np.array_equal(w2.to_coo()[1], exp)
+    u = gb.Vector.from_coo(np.arange(n), sv, dtype=src, size=n)
+    w3 = gb.Vector(getattr(gb, dst), n)
+    assert lib.GrB_Vector_assign(w3._carg, None, None, u._carg, lib.GrB_ALL, n, None) == 0
+    assert np.array_equal(w3.to_coo()[1], exp)
+    w4 = gb.Vector(getattr(gb, dst), n)
+    assert lib.GrB_Vector_apply(w4._carg, None, None, getattr(lib, f"GrB_IDENTITY_{src}"), u._carg, None) == 0
+    assert np.array_equal(w4.to_coo()[1], exp)
