@@ -139,14 +139,17 @@ def _threads():
     return int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
 
 
-def _profile_traffic(name):
-    """HBM bytes per call of a committed per-workload profile (tools/pmc_passes.sh +
-    tools/pmc_table.py: 2 x FETCH_SIZE + WRITE_SIZE summed over the call's kernels)."""
-    path = os.path.join(ROOT, "profiles", name)
-    try:
-        return json.load(open(path))["hbm_bytes_per_call"], f"profiles/{name}"
-    except Exception:
-        return None, None
+def _profile_traffic(*names):
+    """HBM bytes per call of the first committed per-workload profile found among `names`
+    (tools/pmc_passes.sh + tools/pmc_table.py + tools/pmc_percall.py: 2 x FETCH_SIZE + WRITE_SIZE
+    summed over the call's kernels)."""
+    for name in names:
+        path = os.path.join(ROOT, "profiles", name)
+        try:
+            return json.load(open(path))["hbm_bytes_per_call"], f"profiles/{name}"
+        except Exception:
+            continue
+    return None, None
 
 
 def _roofline(alg_bytes, seconds, traffic=None, source=None, kernel=None):
@@ -422,7 +425,8 @@ def config2_spmv(lib, torch, stream, args, scale, ef, O=None, cpu=False):
     parity2 = bool(np.array_equal(present, np.diff(S.tocsc().indptr) > 0) and
                    np.allclose(got, ref, rtol=1e-6, atol=1e-9))
     by = 12 * nnz + 8 * (n + 1) + 16 * n
-    traffic, src = _profile_traffic(f"r03_config2_s{sc}_pmc.json") if ef == 16 else (None, None)
+    traffic, src = _profile_traffic(*([f"r04_config2_s{sc}_pmc.json", f"r03_config2_s{sc}_pmc.json"] if ef == 16 else
+                                      [f"r04_config2_s{sc}_ef{ef}_pmc.json"]))
     res = {
         "workload": f"y = x plus.times A (GrB_vxm, dense fp64 x) on R-MAT s{sc} ef {ef} fp64 U[0,1) "
                     f"(com-Orkut stand-in)",
@@ -508,7 +512,7 @@ def config4_masked_spgemm(lib, torch, stream, O, args, s4, cpu=False):
     by4 = 2 * (12 * nnz4 + 8 * (n4 + 1)) + 4 * nnz4 + 8 * (n4 + 1) + 12 * nnzc + 8 * (n4 + 1)
     for h in (B, C):
         lib.GrB_Matrix_free(ctypes.byref(h))
-    traffic, src = _profile_traffic(f"r03_config4_s{s4}_pmc.json")
+    traffic, src = _profile_traffic(f"r04_config4_s{s4}_pmc.json", f"r03_config4_s{s4}_pmc.json")
     res = {
         "workload": f"C<A.S> = A min.plus A (GrB_mxm, GrB_DESC_S), R-MAT s{s4}, INT64 weights in [1,255]",
         "nnz_A": nnz4, "nnz_C": nnzc, "ms": t4 * 1e3, "gteps": work / t4 / 1e9,

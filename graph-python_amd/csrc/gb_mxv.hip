@@ -1665,6 +1665,15 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             }
             int64_t gcap = gb_knob("iso_work_grid");
             if (gcap <= 0) gcap = iso_work_resident_blocks();
+            // a frontier the host knows to be tiny (the BFS loop reads nvals every level): a small
+            // grid -- the work is a few rows, and the finish's grid-wide sum and the drain of
+            // fewer blocks are what the level costs
+            const int64_t small_n = gb_knob("iso_small_n");
+            if (small_n > 0 && u.h_nvals >= 0 && u.h_nvals <= small_n) {
+                int64_t sg = gb_knob("iso_small_grid");
+                if (sg <= 0) sg = 64;
+                gcap = std::min<int64_t>(gcap, sg);
+            }
             const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 3) / 4, gcap));
             if (grid >= GB_GRID_SHARDS * ((1u << ISO_ARR_BITS) - 1)) args.packed = false;  // arrival field
             GB_HPROF(5, "k_iso_work launch");
