@@ -1026,9 +1026,13 @@ def main():
     # every GrB_vxm / GrB_mxv (k_dir_prep + k_iso_work), one BFS per root
     ev_pairs.clear()
     level_counts.clear()
+    # the events bracket each level's own launch: the library's speculative enqueue of the next
+    # level is switched off for this pass, or a bracket would hold two levels
+    gb.set_knob("bfs_spec", 1)
     for src in roots:
         bfs(src, True)
     torch.cuda.synchronize()
+    gb.set_knob("bfs_spec", 0)
     kern_ms = sum(a.elapsed_time(b) for a, b in ev_pairs)
     launches = len(ev_pairs)
     levels_total = sum(level_counts)

@@ -14,6 +14,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <cstring>
+
 #include "gb_internal.h"
 
 namespace {
@@ -429,6 +431,15 @@ GrB_Info GxB_Global_set_int(const char *key, int64_t value) {
 
 GrB_Info GxB_Global_get_int(const char *key, int64_t *value) {
     if (!key || !value) return GrB_NULL_POINTER;
+    // statistics (read-only): BFS level speculation (gb_ops.hip)
+    if (!strcmp(key, "stat_bfs_spec_adopted")) {
+        *value = g_stat_spec_adopted.load(std::memory_order_relaxed);
+        return GrB_SUCCESS;
+    }
+    if (!strcmp(key, "stat_bfs_spec_rollbacks")) {
+        *value = g_stat_spec_rollbacks.load(std::memory_order_relaxed);
+        return GrB_SUCCESS;
+    }
     *value = gb_knob(key);
     return GrB_SUCCESS;
 }

@@ -165,10 +165,22 @@ void gb_hip_check(hipError_t e, const char *what);
 // other than the SpMV that may fuse it
 extern std::atomic<bool> g_pending_active;
 void gb_pending_flush();
+// a speculatively enqueued next BFS level (gb_ops.hip): rolled back before any API call that
+// could observe it, unless the caller resolves it itself (g_spec_hold > 0); gb_spec_resolve(obj)
+// leaves it in place when obj is a read-only target the speculation does not touch
+extern std::atomic<bool> g_spec_active;
+extern thread_local int g_spec_hold;
+void gb_spec_resolve(const void *keep);
+extern std::atomic<int64_t> g_stat_spec_adopted, g_stat_spec_rollbacks;  // GxB_Global_get_int("stat_...")
+struct gb_spec_hold_guard {
+    gb_spec_hold_guard() { g_spec_hold++; }
+    ~gb_spec_hold_guard() { g_spec_hold--; }
+};
 
 template <bool FLUSH = true, class F>
 GrB_Info gb_api_impl(GB_Obj *errobj, F &&body) {
     try {
+        if (FLUSH && !g_spec_hold && g_spec_active.load(std::memory_order_acquire)) gb_spec_resolve(nullptr);
         if (FLUSH && g_pending_active.load(std::memory_order_acquire)) gb_pending_flush();
         body();
         if (errobj && errobj->magic == GB_MAGIC) errobj->err.clear();

@@ -1155,6 +1155,13 @@ GrB_Info GrB_Matrix_ncols(GrB_Index *n, const GrB_Matrix A) {
 GrB_Info GrB_Matrix_nvals(GrB_Index *n, const GrB_Matrix A) {
     if (!n) return GrB_NULL_POINTER;
     GB_HPROF(7, "GrB_*_nvals (incl. wait)");
+    // a speculated BFS level (gb_ops.hip) changes only its stamp target: counts of anything else
+    // are read without rolling it back
+    if (g_spec_active.load(std::memory_order_acquire)) {
+        GrB_Info e = gb_api_impl<false>(OBJ(A), [&] { gb_spec_resolve(A); });
+        if (e != GrB_SUCCESS) return e;
+    }
+    gb_spec_hold_guard hold;
     return gb_api(OBJ(A), [&] { *n = gb_nvals(gb_obj_check_raw(A)); });
 }
 GrB_Info GrB_Matrix_resize(GrB_Matrix A, GrB_Index nrows, GrB_Index ncols) {

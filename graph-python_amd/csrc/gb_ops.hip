@@ -40,6 +40,60 @@ static bool take_pending_assign(gb_asg &asg, GB_Obj *w, GB_Obj *mask, GB_Obj *A,
                                 bool iso_result);
 
 // ================================================================== mxv / vxm
+// The operand views of one SpMV: A' along the pulled rows (+ the other orientation for the
+// push direction of iso results), u's bitmap (+ its next-frontier edge hint), the mask.
+struct spmv_views {
+    gb_csr_view av, pv;
+    const gb_csr_view *push = nullptr;
+    gb_bitmap_view uv;
+    gb_vmask m;
+    bool iso_result = false;
+};
+
+static void spmv_build_views(spmv_views &V, GB_Obj *mask, GrB_Semiring sr, GB_Obj *A, GB_Obj *u, const gb_desc &d,
+                             bool vxm, int64_t a_rows, const gb_asg *asg) {
+    const bool use_csc = vxm ? !d.tran1 : d.tran0;
+    if (use_csc) gb_get_csc(V.av, A);
+    else gb_get_csr(V.av, A);
+    gb_view_nonempty(V.av, A, use_csc ? 1 : 0);
+    gb_get_bitmap(V.uv, u);
+    if (u->kind != GB_KIND_MATRIX && u->hint_valid) {
+        V.uv.mf_hint = (const long long *)(u->d_nvals + 2);  // GB_HINT_PARTS parts
+        V.uv.hint_key = u->hint_key;
+    }
+    if (u->kind != GB_KIND_MATRIX && u->nvals_valid) V.uv.h_nvals = u->nvals;
+    gb_make_vmask(V.m, mask, d, a_rows);
+    // an empty mask vector: its count is known on the host (value or structure alike)
+    if (V.m.bits && mask && mask->kind != GB_KIND_MATRIX && mask->nvals_valid && mask->nvals == 0) V.m.h_count = 0;
+    // the fused assign's target is the mask (take_pending_assign): its count before this call's
+    // assign, as the host knew it when the assign was deferred (a BFS's first level after
+    // clearing v: 0), lets gb_spmv pick push on the host without the prep launch
+    // -- a stored-entry count equals the set-bit count only for a structural mask; for a value
+    // mask it is an upper bound, which still bounds the open rows of a complemented mask from
+    // below but says nothing for a plain one
+    if (asg && V.m.bits && V.m.h_count < 0 && asg->h_count >= 0 && (d.structure || d.comp))
+        V.m.h_count = asg->h_count;
+    // the other orientation (cached on matrices) enables the push direction for iso results
+    V.iso_result = gb_spmv_result_iso(sr, A->iso, V.uv.iso, vxm);
+    if (!V.iso_result) gb_view_long_rows(V.av, A, use_csc ? 1 : 0);
+    V.uv.full = u->kind != GB_KIND_MATRIX && u->nvals_valid && u->nvals == u->nrows && u->nrows > 0;
+    if (!V.iso_result && V.uv.full && !V.uv.iso && A->kind == GB_KIND_MATRIX && !gb_sr_describe(sr).positional)
+        gb_view_hot(V.av, A, use_csc ? 1 : 0);
+    if (A->kind == GB_KIND_MATRIX && gb_knob("spmv_direction") != 1 && V.iso_result) {
+        if (use_csc) gb_get_csr(V.pv, A);
+        else gb_get_csc(V.pv, A);
+        int64_t H = gb_knob("push_heavy");
+        gb_view_hubs(V.pv, A, use_csc ? 0 : 1, H > 0 ? H : 512);
+        V.push = &V.pv;
+        if (gb_knob("pull_first") != 1) gb_view_pullfirst(V.av, A, use_csc ? 1 : 0, V.pv.rowptr, V.pv.nrows);
+    }
+}
+
+static bool spec_try_adopt(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr, GB_Obj *A, GB_Obj *u,
+                           const gb_desc &d, bool vxm);
+static void spec_after_level(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr, GB_Obj *A, GB_Obj *u,
+                             const gb_desc &d, bool vxm, const gb_asg &asg, bool direct, bool published);
+
 static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr, GB_Obj *A, GB_Obj *u,
                     const gb_desc &d, bool vxm) {
     GB_HPROF(1, "do_spmv total");
@@ -48,11 +102,13 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
     // rows of the operand matrix the kernel pulls along:
     //   mxv:  w = A' u    -> rows of A'          (A' = A: CSR, A' = A^T: CSC)
     //   vxm:  w = u' A'   -> rows of A'^T        (A' = A: CSC, A' = A^T: CSR)
-    bool use_csc = vxm ? !d.tran1 : d.tran0;
     int64_t a_rows = (vxm ? (d.tran1 ? A->nrows : ncols_of(A)) : (d.tran0 ? ncols_of(A) : A->nrows));
     int64_t a_cols = (vxm ? (d.tran1 ? ncols_of(A) : A->nrows) : (d.tran0 ? A->nrows : ncols_of(A)));
     GB_REQUIRE(u->nrows == a_cols && ncols_of(u) == 1, GrB_DIMENSION_MISMATCH, "u size does not match A");
     GB_REQUIRE(w->nrows == a_rows && ncols_of(w) == 1, GrB_DIMENSION_MISMATCH, "w size does not match A");
+    // the next BFS level, launched speculatively by the previous call (below): adopted when this
+    // call is the one predicted, rolled back otherwise
+    if (g_spec_active.load(std::memory_order_acquire) && spec_try_adopt(w, mask, accum, sr, A, u, d, vxm)) return;
     // a deferred `mask<u> = x` (the BFS level stamp) is fused into this call's kernel, or done now
     gb_asg asg;
     bool fused = false;
@@ -62,43 +118,8 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
         if (!fused) gb_pending_flush();
     }
     const int64_t hp_t0 = g_hprof_on ? gb_hprof_now() : 0;
-    gb_csr_view av, pv;
-    if (use_csc) gb_get_csc(av, A);
-    else gb_get_csr(av, A);
-    gb_view_nonempty(av, A, use_csc ? 1 : 0);
-    gb_bitmap_view uv;
-    gb_get_bitmap(uv, u);
-    if (u->kind != GB_KIND_MATRIX && u->hint_valid) {
-        uv.mf_hint = (const long long *)(u->d_nvals + 2);  // GB_HINT_PARTS parts
-        uv.hint_key = u->hint_key;
-    }
-    if (u->kind != GB_KIND_MATRIX && u->nvals_valid) uv.h_nvals = u->nvals;
-    gb_vmask m;
-    gb_make_vmask(m, mask, d, a_rows);
-    // an empty mask vector: its count is known on the host (value or structure alike)
-    if (m.bits && mask && mask->kind != GB_KIND_MATRIX && mask->nvals_valid && mask->nvals == 0) m.h_count = 0;
-    // the fused assign's target is the mask (take_pending_assign): its count before this call's
-    // assign, as the host knew it when the assign was deferred (a BFS's first level after
-    // clearing v: 0), lets gb_spmv pick push on the host without the prep launch
-    // -- a stored-entry count equals the set-bit count only for a structural mask; for a value
-    // mask it is an upper bound, which still bounds the open rows of a complemented mask from
-    // below but says nothing for a plain one
-    if (fused && m.bits && m.h_count < 0 && asg.h_count >= 0 && (d.structure || d.comp)) m.h_count = asg.h_count;
-    // the other orientation (cached on matrices) enables the push direction for iso results
-    const gb_csr_view *push = nullptr;
-    const bool iso_result = gb_spmv_result_iso(sr, A->iso, uv.iso, vxm);
-    if (!iso_result) gb_view_long_rows(av, A, use_csc ? 1 : 0);
-    uv.full = u->kind != GB_KIND_MATRIX && u->nvals_valid && u->nvals == u->nrows && u->nrows > 0;
-    if (!iso_result && uv.full && !uv.iso && A->kind == GB_KIND_MATRIX && !gb_sr_describe(sr).positional)
-        gb_view_hot(av, A, use_csc ? 1 : 0);
-    if (A->kind == GB_KIND_MATRIX && gb_knob("spmv_direction") != 1 && iso_result) {
-        if (use_csc) gb_get_csr(pv, A);
-        else gb_get_csc(pv, A);
-        int64_t H = gb_knob("push_heavy");
-        gb_view_hubs(pv, A, use_csc ? 0 : 1, H > 0 ? H : 512);
-        push = &pv;
-        if (gb_knob("pull_first") != 1) gb_view_pullfirst(av, A, use_csc ? 1 : 0, pv.rowptr, pv.nrows);
-    }
+    spmv_views V;
+    spmv_build_views(V, mask, sr, A, u, d, vxm, a_rows, fused ? &asg : nullptr);
     if (g_hprof_on) gb_hprof_add(2, "do_spmv views+mask", gb_hprof_now() - hp_t0);
     gb_vec_result T;
     if (w->kind != GB_KIND_MATRIX) {
@@ -108,12 +129,13 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
     }
     {
         GB_HPROF(3, "gb_spmv (host+launch)");
-        gb_spmv(T, av, push, uv, m, sr, vxm, fused ? &asg : nullptr);
+        gb_spmv(T, V.av, V.push, V.uv, V.m, sr, vxm, fused ? &asg : nullptr);
     }
     const void *hint_key = T.hint_key;
+    const bool published = T.published;
     GB_HPROF(4, "writeback+epilogue");
     const bool direct = gb_writeback_vector(w, T, mask, d, accum, true);
-    if (direct && T.published) {
+    if (direct && published) {
         // w's count is the one the kernel published; valid until more work is enqueued
         w->pub_seq = T.pub_seq;
         w->pub_epoch = gb_epoch();
@@ -122,6 +144,7 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
         w->hint_valid = true;
         w->hint_key = hint_key;
     }
+    if (fused) spec_after_level(w, mask, accum, sr, A, u, d, vxm, asg, direct, published);
 }
 
 // ================================================================== mxm
@@ -682,6 +705,244 @@ static bool take_pending_assign(gb_asg &asg, GB_Obj *w, GB_Obj *mask, GB_Obj *A,
     return true;
 }
 
+// ---- BFS level speculation (knob bfs_spec = 1 disables).  The notebook's level loop
+// (reference notebooks/Example B.1 cell 8) is
+//     v[:](mask=q.V) << d ;  q(~v.S, replace) << q.vxm(A) ;  if q.nvals == 0: break ;  d += 1
+// and each level's launch waits on the host: the previous level's count reaches the host's
+// nvals, then the host issues the next assign and vxm (≈ 12 µs of idle GPU per level, measured
+// with rocprofv3 kernel traces).  After a level of exactly this shape (the
+// deferred stamp `v<q> = x` fused into `q<!v.S, replace> = q (+).(x) A`, integer x), the next
+// level -- stamp x + 1, then the same SpMV on the q just produced -- is enqueued right behind
+// it, into a result of its own with a mailbox of its own.  When the host then issues exactly
+// that assign and that vxm, the assign is absorbed and the vxm installs the speculative result
+// (and enqueues the level after it): the GPU runs the levels back to back.  Anything else --
+// another call touching v, q or A, a different stamp value, descriptor or semiring -- rolls the
+// speculation back first: the speculative stamp only added q's bits to v (q and v are disjoint:
+// q was produced under the mask !v.S), so clearing q's bits in v and subtracting q's count
+// restores v exactly (nothing to undo when q is empty, the loop's normal exit), the speculative
+// result is dropped, and an absorbed assign is re-issued.  Reads that the speculation leaves
+// alone (nvals of any object but v) go through.  No call ever observes a speculative state.
+std::atomic<bool> g_spec_active{false};
+thread_local int g_spec_hold = 0;
+std::atomic<int64_t> g_stat_spec_adopted{0}, g_stat_spec_rollbacks{0};
+static void vector_assign_scalar(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, const void *x, int xcode,
+                                 const GrB_Index *I, int64_t ni, const gb_desc &d);
+static std::mutex g_spec_mu;
+static struct {
+    bool active = false;
+    GB_Obj *q = nullptr, *v = nullptr, *A = nullptr;  // w == u == q, mask == the stamp's target v
+    GrB_Semiring sr = nullptr;
+    gb_desc d;                     // the SpMV's descriptor
+    bool vxm = false;
+    bool stamp_struct = false;     // the stamp's mask: q.S (true) or q's value (iso q)
+    unsigned long long x = 0;      // the predicted stamp value (v's type, its bytes)
+    gb_vec_result T;               // the speculative next q
+    gb_host_slot *slot = nullptr;  // its mailbox (swapped with q's on adoption)
+    uint64_t *q_bits = nullptr;    // the q the speculative kernel read (and stamped into v)
+    int64_t *q_dn = nullptr;
+    bool assign_matched = false;   // the host has issued the predicted stamp (absorbed)
+} g_spec;
+
+__global__ void k_spec_unstamp(int64_t nw, uint64_t *__restrict__ vbits, const uint64_t *__restrict__ qbits,
+                               int64_t *__restrict__ vcount, const int64_t *__restrict__ qcount) {
+    OPS_STRIDE(k, nw) {
+        const uint64_t qb = qbits[k];
+        if (qb) vbits[k] &= ~qb;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) vcount[0] -= qcount[0];
+}
+
+static bool spec_int_type(int code) { return code >= GBAMD_T_INT8 && code <= GBAMD_T_UINT64; }
+
+static unsigned long long spec_next(unsigned long long x, size_t size) {
+    const unsigned long long m = size >= 8 ? ~0ULL : ((1ULL << (8 * size)) - 1);
+    return (x + 1) & m;  // two's complement wrap in v's width
+}
+
+static void spec_drop_result() {
+    gb_free(g_spec.T.bits);
+    gb_free(g_spec.T.dense);
+    gb_free(g_spec.T.d_nvals);
+    g_spec.T = gb_vec_result{};
+}
+
+// undo the speculative level (g_spec_mu held); see above
+static void spec_rollback_locked() {
+    if (!g_spec.active) return;
+    GB_Obj *q = g_spec.q, *v = g_spec.v;
+    g_spec.active = false;
+    g_spec_active.store(false, std::memory_order_release);
+    g_stat_spec_rollbacks.fetch_add(1, std::memory_order_relaxed);
+    const bool q_empty = q->nvals_valid && q->nvals == 0 && q->bits == g_spec.q_bits;
+    if (!q_empty) {
+        const int64_t nw = gb_words(v->nrows);
+        hipLaunchKernelGGL(k_spec_unstamp, dim3(ops_grid(nw, 1024)), dim3(OPS_BLOCK), 0, gb_stream(), nw, v->bits,
+                           g_spec.q_bits, v->d_nvals, g_spec.q_dn);
+        GB_LAUNCH_CHECK();
+    }
+    spec_drop_result();
+    v->nvals_valid = false;
+    v->hint_valid = false;
+    if (g_spec.assign_matched) {
+        // the host issued the predicted stamp; it was absorbed: issue it now
+        g_spec.assign_matched = false;
+        gb_desc ad;
+        ad.structure = g_spec.stamp_struct;
+        char xc[16] = {0};
+        memcpy(xc, &g_spec.x, sizeof(g_spec.x));
+        vector_assign_scalar(v, q, nullptr, xc, v->type->code, GrB_ALL, v->nrows, ad);
+    }
+}
+
+void gb_spec_resolve(const void *keep) {
+    std::lock_guard<std::mutex> lk(g_spec_mu);
+    if (!g_spec.active) return;
+    if (keep && OBJ(keep) != g_spec.v) return;  // a read the speculation leaves alone
+    spec_rollback_locked();
+}
+
+// enqueue the level after the one just issued (g_spec_mu held): stamp v<q> = x, then
+// q' = q (+).(x) A under !v.S into a result of its own
+static void spec_launch_locked(GB_Obj *q, GB_Obj *v, GB_Obj *A, GrB_Semiring sr, const gb_desc &d, bool vxm,
+                               unsigned long long x, bool stamp_struct) {
+    gb_asg asg;
+    asg.bits = v->bits;
+    asg.vals = v->dense;
+    asg.size = (int)v->type->size;
+    asg.x = x;
+    asg.q_iso = stamp_struct ? nullptr : q->dense;
+    asg.q_iso_code = q->type->code;
+    asg.count = v->d_nvals;
+    asg.h_count = -1;
+    spmv_views V;
+    spmv_build_views(V, v, sr, A, q, d, vxm, q->nrows, &asg);
+    if (!V.iso_result) return;
+    if (!g_spec.slot) g_spec.slot = gb_host_slot_alloc();
+    gb_vec_result T;
+    T.pub = g_spec.slot;
+    T.pub_seq = gb_next_pub_seq();
+    gb_spmv(T, V.av, V.push, V.uv, V.m, sr, vxm, &asg);
+    g_spec.T = T;
+    g_spec.q = q;
+    g_spec.v = v;
+    g_spec.A = A;
+    g_spec.sr = sr;
+    g_spec.d = d;
+    g_spec.vxm = vxm;
+    g_spec.stamp_struct = stamp_struct;
+    g_spec.x = x;
+    g_spec.q_bits = q->bits;
+    g_spec.q_dn = q->d_nvals;
+    g_spec.assign_matched = false;
+    g_spec.active = true;
+    g_spec_active.store(true, std::memory_order_release);
+}
+
+static bool same_desc(const gb_desc &a, const gb_desc &b) {
+    return a.replace == b.replace && a.comp == b.comp && a.structure == b.structure && a.tran0 == b.tran0 &&
+           a.tran1 == b.tran1;
+}
+
+// after a level whose stamp was fused (do_spmv): speculate the next one when the call has the
+// notebook loop's shape
+static void spec_after_level(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr, GB_Obj *A, GB_Obj *u,
+                             const gb_desc &d, bool vxm, const gb_asg &asg, bool direct, bool published) {
+    if (gb_knob("bfs_spec") == 1 || gb_knob("iso_dbg") != 0) return;
+    if (!direct || !published || accum || w != u || !mask || !d.replace || !d.comp || !d.structure) return;
+    if (w->kind == GB_KIND_MATRIX || mask->kind == GB_KIND_MATRIX || A->kind != GB_KIND_MATRIX || A->cw) return;
+    if (!spec_int_type(mask->type->code) || asg.bits != mask->bits || asg.vals != mask->dense) return;
+    std::lock_guard<std::mutex> lk(g_spec_mu);
+    if (g_spec.active) spec_rollback_locked();  // cannot happen (do_spmv adopted or rolled back)
+    try {
+        spec_launch_locked(w, mask, A, sr, d, vxm, spec_next(asg.x, mask->type->size), asg.q_iso == nullptr);
+    } catch (...) {
+        // a speculation that could not be set up is simply not made (the level itself is done);
+        // if its kernel did run, undo it like any other
+        if (g_spec.active) spec_rollback_locked();
+        return;
+    }
+    // the level's own count stays readable from its mailbox: the speculative launch does not touch w
+    if (w->pub_seq) w->pub_epoch = gb_epoch();
+}
+
+// the host issues `w<mask> = x` (all indices, no accum): absorbed when it is the predicted stamp
+static bool spec_match_assign(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, const void *x, int xcode,
+                              const GrB_Index *I, GrB_Descriptor desc) {
+    std::lock_guard<std::mutex> lk(g_spec_mu);
+    if (!g_spec.active) return false;
+    bool ok = !g_spec.assign_matched && w == g_spec.v && mask == g_spec.q && !accum && I == GrB_ALL &&
+              !g_pending_active.load(std::memory_order_acquire) && w->magic == GB_MAGIC;
+    if (ok) {
+        gb_desc ad;
+        try {
+            ad = gb_read_desc(desc);
+        } catch (...) {
+            ok = false;
+        }
+        ok = ok && !ad.replace && !ad.comp && ad.structure == g_spec.stamp_struct && !ad.tran0 && !ad.tran1;
+    }
+    if (ok) {
+        unsigned long long xv = 0;
+        gb_with_type(w->type->code, [&](auto z) {
+            using D = decltype(z);
+            gb_with_type(xcode, [&](auto y) {
+                using S = decltype(y);
+                S sv;
+                memcpy(&sv, x, sizeof(S));
+                D dv = gb_cast<D, S>(sv);
+                memcpy(&xv, &dv, sizeof(D));
+            });
+        });
+        ok = xv == g_spec.x;
+    }
+    if (!ok) {
+        spec_rollback_locked();
+        return false;
+    }
+    g_spec.assign_matched = true;
+    w->err.clear();
+    w->nvals_valid = false;
+    w->hint_valid = false;
+    return true;
+}
+
+// the host issues the predicted SpMV: install the speculative result and speculate again
+static bool spec_try_adopt(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr, GB_Obj *A, GB_Obj *u,
+                           const gb_desc &d, bool vxm) {
+    std::lock_guard<std::mutex> lk(g_spec_mu);
+    if (!g_spec.active) return false;
+    const bool ok = g_spec.assign_matched && w == g_spec.q && u == g_spec.q && mask == g_spec.v && A == g_spec.A &&
+                    sr == g_spec.sr && !accum && vxm == g_spec.vxm && same_desc(d, g_spec.d) &&
+                    w->bits == g_spec.q_bits && g_spec.T.published && gb_knob("bfs_spec") != 1 &&
+                    !g_pending_active.load(std::memory_order_acquire);
+    if (!ok) {
+        spec_rollback_locked();
+        return false;
+    }
+    GB_Obj *q = w, *v = mask;
+    gb_vec_result T = g_spec.T;
+    g_spec.T = gb_vec_result{};
+    g_spec.active = false;
+    g_spec_active.store(false, std::memory_order_release);
+    g_stat_spec_adopted.fetch_add(1, std::memory_order_relaxed);
+    std::swap(q->pub, g_spec.slot);  // the result's mailbox becomes q's; q's old one, the next speculation's
+    const void *hk = T.hint_key;
+    const uint64_t seq = T.pub_seq;
+    gb_writeback_vector(q, T, v, d, nullptr, true);  // replace, T within the mask: installed as is
+    q->pub_seq = seq;
+    q->hint_valid = hk != nullptr;
+    q->hint_key = hk;
+    v->nvals_valid = false;
+    v->hint_valid = false;
+    try {
+        spec_launch_locked(q, v, A, sr, d, vxm, spec_next(g_spec.x, v->type->size), g_spec.stamp_struct);
+    } catch (...) {
+        if (g_spec.active) spec_rollback_locked();
+    }
+    q->pub_epoch = gb_epoch();
+    return true;
+}
+
 static void vector_assign_scalar(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, const void *x, int xcode,
                                  const GrB_Index *I, int64_t ni, const gb_desc &d) {
     check_binop(accum, true);
@@ -1202,6 +1463,9 @@ GrB_Info GrB_Semiring_new(GrB_Semiring *semiring, GrB_Monoid add, GrB_BinaryOp m
     GrB_Info GrB_Vector_assign_##T(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum, ctype x,   \
                                    const GrB_Index *I, GrB_Index ni, const GrB_Descriptor desc) {            \
         GB_HPROF(8, "GrB_Vector_assign scalar");                                                             \
+        if (g_spec_active.load(std::memory_order_acquire) && w && OBJ(w)->magic == GB_MAGIC &&             \
+            spec_match_assign(OBJ(w), mask ? OBJ(mask) : nullptr, accum, &x, GBAMD_T_##T, I, desc))         \
+            return GrB_SUCCESS; /* the predicted level stamp, already carried out (BFS speculation) */     \
         return gb_api(OBJ(w), [&] {                                                                          \
             vector_assign_scalar(gb_obj_check(w), gb_obj_check(mask, true), accum, &x, GBAMD_T_##T, I,       \
                                  (int64_t)ni, gb_read_desc(desc));                                           \

@@ -1,0 +1,278 @@
+"""BFS level speculation (csrc/gb_ops.hip, knob bfs_spec): after a level of the notebook loop
+(reference notebooks/Example B.1 -- Level BFS.ipynb cell 8: `v<q.V> = d; q<!v.S,replace> = q
+(+).(x) A`) the library enqueues the next level behind it and installs that result when the host
+issues exactly the predicted stamp and SpMV; anything else rolls it back first.  These tests drive
+the loop through the C ABI with speculation on (the default) and check that
+
+* the levels equal the oracle's and the speculation was actually adopted (GxB_Global_get_int
+  "stat_bfs_spec_adopted"), for any_pair and lor_land, vxm and mxv, value and structural stamps;
+* every interleaving a caller might do observes no speculative state: reading v mid-loop (nvals,
+  extractTuples), a stamp value other than d + 1, a level without the stamp, a different semiring
+  or descriptor, touching another object;
+and the same with speculation off (knob bfs_spec = 1) gives identical results.
+
+The expected results come from a direct numpy restatement of the loop (any stamp sequence), which
+the oracle's level BFS pins for the plain d = 1, 2, ... loop."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+U64 = ctypes.c_uint64
+
+
+@pytest.fixture(scope="module")
+def gb():
+    import graphblas_amd
+
+    return graphblas_amd
+
+
+@pytest.fixture(scope="module")
+def graph(gb):
+    G = O.rmat(13, 16, 42)
+    r, c, _ = G.to_coo()
+    A = gb.Matrix.from_coo(r, c, True, nrows=G.nrows, ncols=G.ncols)
+    return G, A
+
+
+def stat(gb, key):
+    v = ctypes.c_int64()
+    assert gb.lib.GxB_Global_get_int(key.encode(), ctypes.byref(v)) == 0
+    return v.value
+
+
+def ok(rc, what=""):
+    assert rc == 0, f"{what}: GrB_Info {rc}"
+
+
+def read_vec(lib, v, n):
+    nv = U64()
+    ok(lib.GrB_Vector_nvals(ctypes.byref(nv), v), "nvals")
+    idx = np.empty(nv.value, np.uint64)
+    x = np.empty(nv.value, np.int32)
+    ok(lib.GrB_Vector_extractTuples_INT32(ctypes.c_void_p(idx.ctypes.data), ctypes.c_void_p(x.ctypes.data),
+                                          ctypes.byref(nv), v), "extract")
+    out = np.zeros(n, np.int32)
+    out[idx.astype(np.int64)] = x
+    return out, nv.value
+
+
+def ref_loop(G, src, stamps, mxv=False):
+    """numpy restatement: for level k the stamp value stamps[k] (None: no stamp that level);
+    v<q> = s; q<!v.S, replace> = q (any.pair) A  (vxm: successors; mxv on A: predecessors)"""
+    n = G.nrows
+    rows = np.repeat(np.arange(n), np.diff(G.indptr))
+    v = np.zeros(n, np.int32)
+    have = np.zeros(n, bool)
+    q = np.zeros(n, bool)
+    q[src] = True
+    for s in stamps:
+        if s is not None:
+            v[q] = s
+            have |= q
+        nxt = np.zeros(n, bool)
+        if mxv:  # w(i) = OR_k A(i,k) q(k)
+            nxt[rows[q[G.indices]]] = True
+        else:    # w(j) = OR_i q(i) A(i,j)
+            nxt[G.indices[q[rows]]] = True
+        q = nxt & ~have
+        if not q.any():
+            break
+    return v, q
+
+
+def run_loop(gb, A, n, src, stamps, sr_name="any_pair", mxv=False, stamp_desc=None, hooks=None):
+    """the loop through the C ABI; hooks[k](q, v) runs after level k's nvals"""
+    lib = gb.lib
+    sr = lib.GxB_ANY_PAIR_BOOL if sr_name == "any_pair" else lib.GrB_LOR_LAND_SEMIRING_BOOL
+    q, v = ctypes.c_void_p(), ctypes.c_void_p()
+    ok(lib.GrB_Vector_new(ctypes.byref(q), lib.GrB_BOOL, n))
+    ok(lib.GrB_Vector_new(ctypes.byref(v), lib.GrB_INT32, n))
+    ok(lib.GrB_Vector_setElement_BOOL(q, True, int(src)))
+    nv = U64()
+    for k, s in enumerate(stamps):
+        if s is not None:
+            ok(lib.GrB_Vector_assign_INT32(v, q, None, s, lib.GrB_ALL, n, stamp_desc), "stamp")
+        if mxv:
+            ok(lib.GrB_mxv(q, v, None, sr, A._carg, q, lib.GrB_DESC_RSC), "mxv")
+        else:
+            ok(lib.GrB_vxm(q, v, None, sr, q, A._carg, lib.GrB_DESC_RSC), "vxm")
+        ok(lib.GrB_Vector_nvals(ctypes.byref(nv), q), "nvals q")
+        if hooks and k in hooks:
+            hooks[k](q, v)
+        if nv.value == 0:
+            break
+    got, cnt = read_vec(lib, v, n)
+    qb, _ = read_vec_bool(lib, q, n)
+    lib.GrB_Vector_free(ctypes.byref(q))
+    lib.GrB_Vector_free(ctypes.byref(v))
+    return got, qb
+
+
+def read_vec_bool(lib, q, n):
+    nv = U64()
+    ok(lib.GrB_Vector_nvals(ctypes.byref(nv), q))
+    idx = np.empty(nv.value, np.uint64)
+    x = np.empty(nv.value, np.bool_)
+    ok(lib.GrB_Vector_extractTuples_BOOL(ctypes.c_void_p(idx.ctypes.data), ctypes.c_void_p(x.ctypes.data),
+                                         ctypes.byref(nv), q))
+    out = np.zeros(n, bool)
+    out[idx.astype(np.int64)] = True
+    return out, nv.value
+
+
+def roots(G, k=3):
+    deg = np.diff(G.indptr)
+    return [int(np.argmax(deg)), int(np.flatnonzero(deg > 0)[7]), int(np.flatnonzero(deg > 0)[-3])][:k]
+
+
+@pytest.mark.parametrize("sr_name", ["any_pair", "lor_land"])
+@pytest.mark.parametrize("mxv", [False, True])
+@pytest.mark.parametrize("structural", [False, True])
+def test_spec_levels_match_oracle(gb, graph, sr_name, mxv, structural):
+    G, A = graph
+    n = G.nrows
+    a0 = stat(gb, "stat_bfs_spec_adopted")
+    for src in roots(G):
+        got, q = run_loop(gb, A, n, src, list(range(1, 64)), sr_name, mxv,
+                          gb.lib.GrB_DESC_S if structural else None)
+        if not mxv:
+            ref, _, _ = O.bfs_levels(G, src)
+            assert np.array_equal(got, ref)
+        exp, _ = ref_loop(G, src, list(range(1, 64)), mxv)
+        assert np.array_equal(got, exp) and not q.any()
+    assert stat(gb, "stat_bfs_spec_adopted") > a0, "the speculation was never adopted"
+
+
+def test_spec_off_gives_the_same(gb, graph):
+    G, A = graph
+    src = roots(G)[0]
+    on, _ = run_loop(gb, A, G.nrows, src, list(range(1, 64)))
+    gb.set_knob("bfs_spec", 1)
+    try:
+        a0 = stat(gb, "stat_bfs_spec_adopted")
+        off, _ = run_loop(gb, A, G.nrows, src, list(range(1, 64)))
+        assert stat(gb, "stat_bfs_spec_adopted") == a0
+    finally:
+        gb.set_knob("bfs_spec", 0)
+    assert np.array_equal(on, off)
+
+
+def test_spec_unexpected_stamps(gb, graph):
+    """stamp values other than d + 1 (a repeated value, a jump, a skipped stamp): each breaks
+    the prediction and must roll the speculated level back"""
+    G, A = graph
+    n = G.nrows
+    src = roots(G)[0]
+    for stamps in ([1, 2, 2, 3, 4, 5, 6, 7, 8, 9], [1, 2, 3, 7, 8, 9, 10, 11, 12], [1, 2, None, 3, 4, 5, 6, 7, 8],
+                   [5, 4, 3, 2, 1, 0, -1, -2, -3]):
+        r0 = stat(gb, "stat_bfs_spec_rollbacks")
+        got, q = run_loop(gb, A, n, src, stamps)
+        exp, eq = ref_loop(G, src, stamps)
+        assert np.array_equal(got, exp), stamps
+        assert np.array_equal(q, eq), stamps
+        assert stat(gb, "stat_bfs_spec_rollbacks") > r0
+
+
+def test_spec_reads_and_writes_mid_loop(gb, graph):
+    """nvals / extractTuples of v between levels (v carries the speculative stamp until the
+    rollback), a read of an unrelated object (no rollback needed) and an assign to it"""
+    G, A = graph
+    n = G.nrows
+    lib = gb.lib
+    src = roots(G)[0]
+    ref, _, _ = O.bfs_levels(G, src)
+    seen = {}
+
+    def read_v(q, v):
+        got, cnt = read_vec(lib, v, n)
+        seen[len(seen)] = (got.copy(), cnt)
+
+    other = ctypes.c_void_p()
+    ok(lib.GrB_Vector_new(ctypes.byref(other), lib.GrB_INT64, n))
+
+    def touch_other(q, v):
+        nv = U64()
+        ok(lib.GrB_Vector_nvals(ctypes.byref(nv), other))
+        ok(lib.GrB_Vector_assign_INT64(other, None, None, 7, lib.GrB_ALL, n, None))
+
+    hooks = {1: read_v, 2: touch_other, 3: read_v}
+    got, _ = run_loop(gb, A, n, src, list(range(1, 64)), hooks=hooks)
+    assert np.array_equal(got, ref)
+    # what v held after levels 2 and 4 (hooks 1 and 3): the stamps up to that level only
+    for (lv, cnt), lvl in zip(seen.values(), (2, 4)):
+        exp = np.where((ref > 0) & (ref <= lvl), ref, 0)
+        assert np.array_equal(lv, exp) and cnt == int((exp > 0).sum())
+    lib.GrB_Vector_free(ctypes.byref(other))
+
+
+def test_spec_other_call_between_stamp_and_spmv(gb, graph):
+    """the predicted stamp is issued (absorbed), then another call reads v before the SpMV: the
+    rollback re-issues the absorbed stamp, so v holds it"""
+    G, A = graph
+    n = G.nrows
+    lib = gb.lib
+    src = roots(G)[0]
+    sr = lib.GxB_ANY_PAIR_BOOL
+    q, v = ctypes.c_void_p(), ctypes.c_void_p()
+    ok(lib.GrB_Vector_new(ctypes.byref(q), lib.GrB_BOOL, n))
+    ok(lib.GrB_Vector_new(ctypes.byref(v), lib.GrB_INT32, n))
+    ok(lib.GrB_Vector_setElement_BOOL(q, True, src))
+    nv = U64()
+    ref, _, _ = O.bfs_levels(G, src)
+    d = 0
+    while True:
+        d += 1
+        ok(lib.GrB_Vector_assign_INT32(v, q, None, d, lib.GrB_ALL, n, None))
+        if d == 3:
+            got, cnt = read_vec(lib, v, n)  # v after the level-3 stamp, before the SpMV
+            exp = np.where((ref > 0) & (ref <= 3), ref, 0)
+            assert np.array_equal(got, exp) and cnt == int((exp > 0).sum())
+        ok(lib.GrB_vxm(q, v, None, sr, q, A._carg, lib.GrB_DESC_RSC))
+        ok(lib.GrB_Vector_nvals(ctypes.byref(nv), q))
+        if nv.value == 0:
+            break
+    got, _ = read_vec(lib, v, n)
+    assert np.array_equal(got, ref)
+    lib.GrB_Vector_free(ctypes.byref(q))
+    lib.GrB_Vector_free(ctypes.byref(v))
+
+
+def test_spec_changed_call_shape(gb, graph):
+    """the predicted stamp, then an SpMV that differs from the prediction (another semiring, a
+    non-replace descriptor): rolled back, the absorbed stamp re-issued, results as without
+    speculation"""
+    G, A = graph
+    n = G.nrows
+    lib = gb.lib
+    src = roots(G)[0]
+    for variant in ("semiring", "descriptor"):
+        results = []
+        for spec in (0, 1):
+            gb.set_knob("bfs_spec", spec)
+            q, v = ctypes.c_void_p(), ctypes.c_void_p()
+            ok(lib.GrB_Vector_new(ctypes.byref(q), lib.GrB_BOOL, n))
+            ok(lib.GrB_Vector_new(ctypes.byref(v), lib.GrB_INT32, n))
+            ok(lib.GrB_Vector_setElement_BOOL(q, True, src))
+            nv = U64()
+            for d in range(1, 7):
+                ok(lib.GrB_Vector_assign_INT32(v, q, None, d, lib.GrB_ALL, n, None))
+                sr, desc = lib.GxB_ANY_PAIR_BOOL, lib.GrB_DESC_RSC
+                if d == 3:
+                    if variant == "semiring":
+                        sr = lib.GrB_LOR_LAND_SEMIRING_BOOL
+                    else:
+                        desc = lib.GrB_DESC_SC
+                ok(lib.GrB_vxm(q, v, None, sr, q, A._carg, desc))
+                ok(lib.GrB_Vector_nvals(ctypes.byref(nv), q))
+                if nv.value == 0:
+                    break
+            results.append((read_vec(lib, v, n)[0], read_vec_bool(lib, q, n)[0]))
+            lib.GrB_Vector_free(ctypes.byref(q))
+            lib.GrB_Vector_free(ctypes.byref(v))
+        gb.set_knob("bfs_spec", 0)
+        assert np.array_equal(results[0][0], results[1][0]) and np.array_equal(results[0][1], results[1][1])
