@@ -456,10 +456,17 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
     const Z ident = ANY ? Z() : gb_monoid_identity<Z>(mon);
     const unsigned long long ltmask = (1ULL << lane) - 1;
     int32_t *stg = stage[wid];
-    for (int64_t t = blockIdx.x; t < ntask; t += gridDim.x) {
+    // a contiguous run of tasks per workgroup (tasks are cut to similar cost, so runs balance):
+    // consecutive tasks of one group share X(g,:), whose keys and filter then stay in LDS
+    const int64_t per = (ntask + gridDim.x - 1) / gridDim.x;
+    const int64_t t_end = min(ntask, (int64_t)(blockIdx.x + 1) * per);
+    int64_t prev_g = -1;
+    for (int64_t t = (int64_t)blockIdx.x * per; t < t_end; t++) {
         const int64_t e0 = tstart[t];
         const int ne = __builtin_amdgcn_readfirstlane((int)(tstart[t + 1] - e0));
         const int64_t g = eG[e0];
+        const bool reuse = g == prev_g && !(dbg & 64);  // dbg 64: reload X every task (A/B)
+        prev_g = g;
         int64_t xs = s.xrp[g];
         int64_t alen = s.xrp[g + 1] - xs;
         if (piece >= 0) {  // piece `piece` of a list longer than the cap
@@ -468,7 +475,8 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
             if (alen > pcap) alen = pcap;
         }
         const int a = __builtin_amdgcn_readfirstlane((int)alen);
-        for (int i = tid; i < (1 << (DT_FLOG - 5)); i += DT_TB) filt[i] = 0;
+        if (!reuse)
+            for (int i = tid; i < (1 << (DT_FLOG - 5)); i += DT_TB) filt[i] = 0;
         for (int i = tid; i < DT_SMAX / 64 + 1; i += DT_TB) estart[i] = 0;
         int b = 0;
         if (tid < ne) {
@@ -490,12 +498,13 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
         if (lane == 63) w_sum[wid] = inc;
         if (tid == 0) next_unit = 0;
         __syncthreads();  // filter and start bits cleared, wave sums visible
-        for (int i = tid; i < a; i += DT_TB) {
-            const int32_t k = s.xci[xs + i];
-            keys[i] = k;
-            const uint32_t h = dt_hash(k);
-            atomicOr(&filt[h >> 5], 1u << (h & 31));
-        }
+        if (!reuse)
+            for (int i = tid; i < a; i += DT_TB) {
+                const int32_t k = s.xci[xs + i];
+                keys[i] = k;
+                const uint32_t h = dt_hash(k);
+                atomicOr(&filt[h >> 5], 1u << (h & 31));
+            }
         int base = 0, S = 0;
         for (int w = 0; w < DT_TB / 64; w++) {
             if (w < wid) base += w_sum[w];

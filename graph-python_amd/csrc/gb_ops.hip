@@ -740,11 +740,17 @@ static struct {
     gb_host_slot *slot = nullptr;  // its mailbox (swapped with q's on adoption)
     uint64_t *q_bits = nullptr;    // the q the speculative kernel read (and stamped into v)
     int64_t *q_dn = nullptr;
+    const void *q_iso = nullptr;   // its iso value (a value-mask stamp happens only when nonzero)
+    int q_iso_code = 0;
     bool assign_matched = false;   // the host has issued the predicted stamp (absorbed)
 } g_spec;
 
+// q_iso: q's iso value when the stamp's mask was q's values (nullptr: q.S) -- an iso-false q
+// stamped nothing, so there is nothing to take back
 __global__ void k_spec_unstamp(int64_t nw, uint64_t *__restrict__ vbits, const uint64_t *__restrict__ qbits,
-                               int64_t *__restrict__ vcount, const int64_t *__restrict__ qcount) {
+                               int64_t *__restrict__ vcount, const int64_t *__restrict__ qcount, const void *q_iso,
+                               int q_iso_code) {
+    if (q_iso && !gb_dyn_nonzero(q_iso, q_iso_code)) return;
     OPS_STRIDE(k, nw) {
         const uint64_t qb = qbits[k];
         if (qb) vbits[k] &= ~qb;
@@ -777,7 +783,8 @@ static void spec_rollback_locked() {
     if (!q_empty) {
         const int64_t nw = gb_words(v->nrows);
         hipLaunchKernelGGL(k_spec_unstamp, dim3(ops_grid(nw, 1024)), dim3(OPS_BLOCK), 0, gb_stream(), nw, v->bits,
-                           g_spec.q_bits, v->d_nvals, g_spec.q_dn);
+                           g_spec.q_bits, v->d_nvals, g_spec.q_dn, g_spec.stamp_struct ? nullptr : g_spec.q_iso,
+                           g_spec.q_iso_code);
         GB_LAUNCH_CHECK();
     }
     spec_drop_result();
@@ -833,6 +840,8 @@ static void spec_launch_locked(GB_Obj *q, GB_Obj *v, GB_Obj *A, GrB_Semiring sr,
     g_spec.x = x;
     g_spec.q_bits = q->bits;
     g_spec.q_dn = q->d_nvals;
+    g_spec.q_iso = q->dense;
+    g_spec.q_iso_code = q->type->code;
     g_spec.assign_matched = false;
     g_spec.active = true;
     g_spec_active.store(true, std::memory_order_release);
