@@ -435,7 +435,7 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
     int64_t ntask, const int64_t *__restrict__ tstart, const int32_t *__restrict__ eG,
     const int64_t *__restrict__ eYS, const int32_t *__restrict__ eO, const int32_t *__restrict__ eB,
     const int64_t *__restrict__ eQ, Z *__restrict__ tval, uint8_t *__restrict__ tflag, int dbg, int piece,
-    int pcap) {
+    int pcap, unsigned long long *__restrict__ tctr, int chunk) {
     __shared__ int32_t keys[DT_CAP];
     __shared__ uint32_t filt[1 << (DT_FLOG - 5)];
     __shared__ uint64_t estart[DT_SMAX / 64 + 1];     // bit f: an entry starts at flat element f
@@ -456,12 +456,19 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
     const Z ident = ANY ? Z() : gb_monoid_identity<Z>(mon);
     const unsigned long long ltmask = (1ULL << lane) - 1;
     int32_t *stg = stage[wid];
-    // a contiguous run of tasks per workgroup (tasks are cut to similar cost, so runs balance):
-    // consecutive tasks of one group share X(g,:), whose keys and filter then stay in LDS
-    const int64_t per = (ntask + gridDim.x - 1) / gridDim.x;
-    const int64_t t_end = min(ntask, (int64_t)(blockIdx.x + 1) * per);
+    // tasks are handed out in chunks of `chunk` consecutive tasks from a grid-wide counter
+    // (dynamic: the workgroups stay balanced); consecutive tasks of one group share X(g,:),
+    // whose keys and filter then stay in LDS
+    __shared__ int64_t s_chunk;
     int64_t prev_g = -1;
-    for (int64_t t = (int64_t)blockIdx.x * per; t < t_end; t++) {
+    for (;;) {
+    if (tid == 0) s_chunk = (int64_t)atomicAdd(tctr, (unsigned long long)chunk);
+    __syncthreads();
+    const int64_t c0 = s_chunk;
+    __syncthreads();  // every thread has read the chunk before it is rewritten
+    if (c0 >= ntask) break;
+    const int64_t c1 = c0 + chunk < ntask ? c0 + chunk : ntask;
+    for (int64_t t = c0; t < c1; t++) {
         const int64_t e0 = tstart[t];
         const int ne = __builtin_amdgcn_readfirstlane((int)(tstart[t + 1] - e0));
         const int64_t g = eG[e0];
@@ -633,6 +640,7 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
         }
         __syncthreads();
     }
+    }
 }
 
 }  // namespace
@@ -722,12 +730,16 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
                 hipLaunchKernelGGL(k_dt_task_fill, dim3(dt_grid(ne)), dim3(DT_BLOCK), 0, gb_stream(), ne, tsf, tpos,
                                    tstart);
                 GB_LAUNCH_CHECK();
-                // persistent workgroups: one per CU
+                // persistent workgroups (two per CU) taking chunks of consecutive tasks
                 const unsigned gt = (unsigned)std::min<int64_t>(nt, 1024);
+                unsigned long long *tctr = ts.get<unsigned long long>(1);
+                gb_memset(tctr, 0, sizeof(unsigned long long));
+                int64_t chunk = gb_knob("dot_chunk");
+                if (chunk <= 0) chunk = 8;
                 if (!(skip & 2))
                     hipLaunchKernelGGL((k_dot_task<SRT, X, Z, SWAP>), dim3(gt), dim3(DT_TB), 0, gb_stream(), srf,
                                        info.mon, sd, xv, xiso, yv, yiso, nt, tstart, eG, eYS, eO, eB, eQ, (Z *)tval,
-                                       tflag, (int)gb_knob("dot_dbg"), piece, cap);
+                                       tflag, (int)gb_knob("dot_dbg"), piece, cap, tctr, (int)chunk);
                 GB_LAUNCH_CHECK();
             };
             gb_exclusive_scan_u8(tf, pos, nm);
