@@ -734,8 +734,10 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
                 const unsigned gt = (unsigned)std::min<int64_t>(nt, 1024);
                 unsigned long long *tctr = ts.get<unsigned long long>(1);
                 gb_memset(tctr, 0, sizeof(unsigned long long));
+                // tools/spgemm_probe.py (R-MAT, one box): chunk 1/4/8/16/32 -> s20 24.7/24.1/25.3/27.7/33.0 ms,
+                // s22 (1/8/32) 128.6/121.5/136.3 ms
                 int64_t chunk = gb_knob("dot_chunk");
-                if (chunk <= 0) chunk = 8;
+                if (chunk <= 0) chunk = 4;
                 if (!(skip & 2))
                     hipLaunchKernelGGL((k_dot_task<SRT, X, Z, SWAP>), dim3(gt), dim3(DT_TB), 0, gb_stream(), srf,
                                        info.mon, sd, xv, xiso, yv, yiso, nt, tstart, eG, eYS, eO, eB, eQ, (Z *)tval,

@@ -14,6 +14,7 @@
 #                         -> gpurun_out/NAME/ + top kernels (tools/kstats.py)
 #   prof:NAME:CMD         the same for CMD (comma-separated argv: a script under the repo root + args)
 #   pmc:NAME:REGEX:CMD    tools/pmc_passes.sh NAME REGEX CMD (trace + FETCH / WRITE / TCC / SQ passes)
+#   pmck:NAME:REGEX:CMD   tools/pmc_kernel.sh NAME REGEX CMD (instruction mix, LDS, waits, L2, FETCH)
 #   py:CMD                python3 CMD (comma-separated argv), 300 s limit
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(pwd)}"
@@ -65,6 +66,10 @@ for step in "$@"; do
     name=${rest%%:*}; r2=${rest#*:}; regex=${r2%%:*}; cmd=${r2#*:}
     argv=(${cmd//,/ })
     bash tools/pmc_passes.sh "$name" "$regex" python3 "$R/${argv[0]}" "${argv[@]:1}" || exit 1 ;;
+  pmck)
+    name=${rest%%:*}; r2=${rest#*:}; regex=${r2%%:*}; cmd=${r2#*:}
+    argv=(${cmd//,/ })
+    bash tools/pmc_kernel.sh "$name" "$regex" python3 "$R/${argv[0]}" "${argv[@]:1}" || exit 1 ;;
   py)
     timeout -k 10 300 python3 ${rest//,/ } || exit 1 ;;
   *)
