@@ -1273,7 +1273,12 @@ void spgemm_hash_run(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, const gb_
             // numeric windows sized for two 1024-thread workgroups per CU (round 3: 2^17 columns,
             // 8192 LDS values and 4 products per thread held one workgroup of 153 KB LDS per
             // CU at 4 waves per SIMD; config 5 s19 219 -> 204 ms at 2^16 / 3072 / 2, <= 64 VGPRs)
-            const int lw = SYM ? win_log(19) : (sizeof(Z) < 4 ? std::max(9, win_log(13)) : win_log(16));
+            int lw = SYM ? win_log(19) : (sizeof(Z) < 4 ? std::max(9, win_log(13)) : win_log(16));
+            // knob window_lw (numeric, 4-8-byte values): wider windows, fewer sweeps of a row's A
+            // entries per row (one workgroup per CU above 2^16 columns: the bitmap and its
+            // prefix take W/4 bytes of LDS)
+            const int64_t klw = gb_knob("window_lw");
+            if (!SYM && sizeof(Z) >= 4 && klw >= 10 && klw <= 18) lw = win_log((int)klw);
             int vcap = (SYM || !VALS) ? 0 : (sizeof(Z) < 4 ? (1 << lw) : 3072);
             // tests: a small LDS value capacity sends windows to the C-resident accumulation
             const int64_t kv = gb_knob("window_vcap");
