@@ -60,7 +60,7 @@ def parse():
     p.add_argument("--no-msbfs-sharded", action="store_true",
                    help="N > 1: skip the row-sharded 64-root BFS line (one exchange per level for 64 roots)")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
-    p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
+    p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r04.json"))
     # rehearsal of the N>1 path on one GPU: all ranks on one device, gloo transport
     p.add_argument("--dist-backend", default="nccl")
     p.add_argument("--partition", default="balanced", choices=["balanced", "equal"],
@@ -520,7 +520,12 @@ def config4_masked_spgemm(lib, torch, stream, O, args, s4, cpu=False):
         "intersection_keys_per_s": inter / t4,
         "intersection_def": "sum over mask entries of min(deg_out(i), deg_in(j)): the keys the dot streams",
         "alg_bytes": by4, "hbm_GBs": by4 / t4 / 1e9, "parity_vs_oracle_256_rows": parity4,
-        "roofline": _roofline(by4, t4, traffic, src, "masked dot kernels (k_dot_task, k_dot_small, ...; one call)")}
+        "roofline": _roofline(by4, t4, traffic, src, "masked dot kernels (k_dot_task, k_dot_small, ...; one call)"),
+        # the dot form's own floor: every mask entry streams its shorter list once (4-byte keys;
+        # SURVEY 8(d)'s compulsory bytes beside it) -- the bytes the method cannot avoid
+        "roofline_dot_floor": dict(_roofline(by4 + 4 * inter, t4, traffic, src, "the same call"),
+                                   alg_bytes_def="SURVEY 8(d) config 4 bytes + 4 B x sum over mask entries of "
+                                                 "min(deg_out(i), deg_in(j)) (each shorter list streamed once)")}
     if cpu and not args.no_cpu_baseline:
         # the masked dot on all host cores (oracle or_masked_dot_min_plus_int64_par: per mask entry a
         # sorted merge / galloping of A(i,:) with A(:,j)) over the mask rows [0, r1) -- labels are
@@ -1178,6 +1183,10 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": (achieved / PEAK_HBM_GBS) if achieved else None, "traffic": traffic,
                          "kernel": "k_iso_work (+ k_dir_prep on a BFS's first level)",
+                         "rocprof_note": "timed with the level speculation off (one launch per level); under "
+                                         "rocprofv3 the speculating loop shows one more, empty k_iso_work per BFS "
+                                         "(the level after the last) -- profiles/r04_bfs_nospec_kernel_stats.csv "
+                                         "is the BFS with bfs_spec=1, whose average is this one's",
                          "avg_launch_us": kern_ms * 1e3 / launches,
                          "launches": launches, "alg_bytes_per_launch": alg_bytes / launches,
                          "stream_copy_GBs": copy_gbs},

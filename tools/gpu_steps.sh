@@ -16,6 +16,7 @@
 #   pmc:NAME:REGEX:CMD    tools/pmc_passes.sh NAME REGEX CMD (trace + FETCH / WRITE / TCC / SQ passes)
 #   pmck:NAME:REGEX:CMD   tools/pmc_kernel.sh NAME REGEX CMD (instruction mix, LDS, waits, L2, FETCH)
 #   py:CMD                python3 CMD (comma-separated argv), 300 s limit
+#   pyx:CMD               the same with ~ separating the arguments (arguments that hold commas)
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(pwd)}"
 cd "$R" || exit 1
@@ -72,6 +73,9 @@ for step in "$@"; do
     bash tools/pmc_kernel.sh "$name" "$regex" python3 "$R/${argv[0]}" "${argv[@]:1}" || exit 1 ;;
   py)
     timeout -k 10 300 python3 ${rest//,/ } || exit 1 ;;
+  pyx)
+    IFS='~' read -r -a argv <<< "$rest"
+    timeout -k 10 300 python3 "${argv[@]}" || exit 1 ;;
   *)
     echo "unknown step $step"; exit 2 ;;
   esac

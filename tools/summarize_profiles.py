@@ -28,7 +28,11 @@ def means(path):
 
 fetch = means(os.path.join(src, "pmc_fetch", "bench_counter_collection.csv"))
 write = means(os.path.join(src, "pmc_write", "bench_counter_collection.csv"))
-stats = {r["Name"].split("(")[0]: r for r in csv.DictReader(open(os.path.join(src, "prof_stats", "bench_kernel_stats.csv")))}
+# per-launch durations from the run the PMC passes repeat (speculation off: one launch per level)
+sdir = "prof_stats_nospec" if os.path.isdir(os.path.join(src, "prof_stats_nospec")) else "prof_stats"
+if sdir == "prof_stats_nospec":
+    shutil.copy(os.path.join(src, sdir, "bench_kernel_stats.csv"), os.path.join(dst, f"{rnd}_bfs_nospec_kernel_stats.csv"))
+stats = {r["Name"].split("(")[0]: r for r in csv.DictReader(open(os.path.join(src, sdir, "bench_kernel_stats.csv")))}
 lines = ["kernel,launches,avg_us,FETCH_SIZE_KiB_mean,WRITE_SIZE_KiB_mean,hbm_bytes_per_launch_corrected"]
 out = {}
 for (kname, _), (cnt, fkib) in fetch.items():
