@@ -1033,11 +1033,12 @@ def main():
     level_counts.clear()
     # the events bracket each level's own launch: the library's speculative enqueue of the next
     # level is switched off for this pass, or a bracket would hold two levels
+    spec_knob = gb.get_knob("bfs_spec")
     gb.set_knob("bfs_spec", 1)
     for src in roots:
         bfs(src, True)
     torch.cuda.synchronize()
-    gb.set_knob("bfs_spec", 0)
+    gb.set_knob("bfs_spec", spec_knob)
     kern_ms = sum(a.elapsed_time(b) for a, b in ev_pairs)
     launches = len(ev_pairs)
     levels_total = sum(level_counts)

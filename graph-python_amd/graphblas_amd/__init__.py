@@ -55,6 +55,14 @@ def set_knob(key, value):
     lib.GxB_Global_set_int(key.encode(), int(value))
 
 
+def get_knob(key):
+    """A library knob's value (GxB_Global_get_int; 0 when unset), or a read-only statistic
+    ("stat_bfs_spec_adopted", "stat_bfs_spec_rollbacks")."""
+    v = ctypes.c_int64()
+    lib.GxB_Global_get_int(key.encode(), ctypes.byref(v))
+    return v.value
+
+
 def wait():
     """Block until all queued device work is complete."""
     s = Scalar(BOOL)

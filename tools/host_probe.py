@@ -31,6 +31,7 @@ nv = ctypes.c_uint64()
 sr, desc, ALL = lib.GrB_LOR_LAND_SEMIRING_BOOL, lib.GrB_DESC_RSC, lib.GrB_ALL
 f_assign, f_vxm, f_nvals = lib.GrB_Vector_assign_INT32, lib.GrB_vxm, lib.GrB_Vector_nvals
 tot = {"assign": [], "vxm": [], "nvals": [], "loop": []}
+last = []
 for rep in range(20):
     lib.GrB_Vector_clear(q)
     lib.GrB_Vector_clear(v)
@@ -50,12 +51,17 @@ for rep in range(20):
             tot["assign"].append(t1 - t0)
             tot["vxm"].append(t2 - t1)
             tot["nvals"].append(t3 - t2)
+        if rep == 19:
+            last.append((d, t1 - t0, t2 - t1, t3 - t2, nv.value))
         if nv.value == 0:
             break
 for k, xs in tot.items():
     if xs:
         a = np.array(xs) * 1e6
         print(f"{k:7s} median {np.median(a):7.1f} us  p10 {np.percentile(a, 10):7.1f}  p90 {np.percentile(a, 90):7.1f}  n={a.size}")
+print("last BFS per level (us): level assign vxm nvals | frontier")
+for d_, a_, b_, c_, f_ in last:
+    print(f"  {d_:2d} {a_ * 1e6:7.1f} {b_ * 1e6:7.1f} {c_ * 1e6:7.1f} | {f_}")
 # empty C call for ctypes overhead
 t0 = time.perf_counter()
 for _ in range(10000):
