@@ -118,21 +118,25 @@ gb_host_slot *gb_host_slot_device(gb_host_slot *s) {
 
 uint64_t gb_next_pub_seq() { return g_pub_seq.fetch_add(1, std::memory_order_relaxed) + 1; }
 
+static inline bool slot_match(gb_host_slot *s, uint64_t seq, int64_t *value) {
+    const uint64_t w = (uint64_t)__atomic_load_n(&s->seq, __ATOMIC_ACQUIRE);
+    if (w == seq) {
+        *value = __atomic_load_n(&s->value, __ATOMIC_RELAXED);
+        return true;
+    }
+    if ((w & GB_PUB_TAG) && ((w >> 32) & 0x7fffffffULL) == (seq & 0x7fffffffULL)) {
+        *value = (int64_t)(w & 0xffffffffULL);  // tagged one-word publish
+        return true;
+    }
+    return false;
+}
+
 bool gb_host_slot_wait(gb_host_slot *s, uint64_t seq, int64_t *value) {
     for (uint64_t i = 1;; i++) {
-        if ((uint64_t)__atomic_load_n(&s->seq, __ATOMIC_ACQUIRE) == seq) {
-            *value = __atomic_load_n(&s->value, __ATOMIC_RELAXED);
-            return true;
-        }
+        if (slot_match(s, seq, value)) return true;
         if ((i & 1023) == 0) {
             hipError_t q = hipStreamQuery(gb_stream_peek());
-            if (q != hipErrorNotReady) {  // drained (or failed): one last look
-                if ((uint64_t)__atomic_load_n(&s->seq, __ATOMIC_ACQUIRE) == seq) {
-                    *value = __atomic_load_n(&s->value, __ATOMIC_RELAXED);
-                    return true;
-                }
-                return false;
-            }
+            if (q != hipErrorNotReady) return slot_match(s, seq, value);  // drained (or failed): one last look
         }
         __builtin_ia32_pause();
     }
@@ -438,6 +442,11 @@ GrB_Info GxB_Global_get_int(const char *key, int64_t *value) {
     }
     if (!strcmp(key, "stat_bfs_spec_rollbacks")) {
         *value = g_stat_spec_rollbacks.load(std::memory_order_relaxed);
+        return GrB_SUCCESS;
+    }
+    // vector counts read with a device copy (stream sync) instead of the kernel's mailbox
+    if (!strcmp(key, "stat_nvals_copy")) {
+        *value = g_stat_nvals_copy.load(std::memory_order_relaxed);
         return GrB_SUCCESS;
     }
     *value = gb_knob(key);

@@ -39,9 +39,10 @@ constexpr int DT_BLOCK = 256;
 constexpr int DT_SMALL = 64;      // long side <= 64: k_dot_small, keys one per lane
 constexpr int DT_MID = 256;       // long side <= 256: k_dot_small, four keys per lane
 constexpr int DT_CAP = 8192;      // long side <= DT_CAP: k_dot_task (keys in LDS)
-constexpr int DT_OVH = 256;       // per-entry cost added to the streamed length (task windows)
-constexpr int DT_WIN = 32768;     // task window: <= DT_WIN / DT_OVH entries start in one
-constexpr int DT_MAXE = DT_WIN / DT_OVH;
+constexpr int DT_OVH = 128;       // per-entry cost added to the streamed length (task windows)
+constexpr int DT_OVH_MIN = 128;   // the least per-entry cost (knob dot_ovh): sizes the task's entry arrays
+constexpr int DT_WIN = 32768;     // task window: <= DT_WIN / ovh entries start in one
+constexpr int DT_MAXE = DT_WIN / DT_OVH_MIN;
 
 static inline unsigned dt_grid(int64_t n, int per_block = DT_BLOCK, int64_t cap = 1 << 16) {
     int64_t g = (n + per_block - 1) / per_block;
@@ -547,31 +548,43 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
             int cur_e = -1;
             bool found = false;
             Z acc = Z();
+            // one step's key loads (DT_U windows of 64 flat elements from fb): the entries
+            // starting in each window (all windows' words read at once; the entry before each
+            // window follows from the previous words' popcounts, so no window waits on another's
+            // cross-lane step), the lanes' entries, then the loads back to back.  Measured
+            // neutral against the round-4 per-window chain, and so was issuing the next step's
+            // loads before this step's search (software pipelining): 118.5 vs 118.8 ms at s22
+            auto issue = [&](int fb, int (&ee_o)[DT_U], int32_t (&k_o)[DT_U]) {
+                uint64_t sb[DT_U];
+#pragma unroll
+                for (int u = 0; u < DT_U; u++) sb[u] = estart[(fb >> 6) + u];
+#pragma unroll
+                for (int u = 0; u < DT_U; u++) {
+                    // a start at the window's first element is counted by the popcount
+                    // (ew holds the entry of the element before it)
+                    const int ustart = (fb + u * 64 == fu0 && (sb[u] & 1ULL)) ? 1 : 0;  // unit start: ew is it
+                    ee_o[u] = ew + __popcll(sb[u] & ((ltmask << 1) | 1ULL)) - ustart;
+                    ew = __builtin_amdgcn_readfirstlane(ew + __popcll(sb[u]) - ustart);  // lane 63's entry
+                }
+                int64_t py[DT_U];
+#pragma unroll
+                for (int u = 0; u < DT_U; u++) {
+                    const int f = fb + u * 64 + lane;
+                    const int eL = ee_o[u] < ne ? ee_o[u] : ne - 1;
+                    py[u] = f < fu1 ? e_ys[eL] + (f - e_pre[eL]) : 0;  // past the unit: a harmless load
+                }
+#pragma unroll
+                for (int u = 0; u < DT_U; u++) k_o[u] = s.yci[py[u]];
+            };
             for (int f0 = fu0; f0 < ((dbg & 8) ? fu0 : fu1); f0 += 64 * DT_U) {
                 int cnt = 0;
                 int32_t k[DT_U];
                 int ee[DT_U];
-                int64_t py[DT_U];
-#pragma unroll
-                for (int u = 0; u < DT_U; u++) {
-                    // entries starting in this 64-element window, then the lane's entry
-                    const int fw = f0 + u * 64;
-                    const uint64_t sb = estart[fw >> 6];
-                    const int f = fw + lane;
-                    // a start at the window's first element is counted by the popcount
-                    // (ew holds the entry of the element before it)
-                    int e_l = ew + __popcll(sb & ((ltmask << 1) | 1ULL));
-                    if (fw == fu0 && (sb & 1ULL)) e_l -= 1;  // unit start: ew already is that entry
-                    ee[u] = e_l;
-                    const int eL = e_l < ne ? e_l : ne - 1;
-                    py[u] = e_ys[eL] + (f - e_pre[eL]);
-                    ew = __builtin_amdgcn_readfirstlane(__shfl(e_l, 63, 64));
-                    k[u] = f < fu1 ? ((dbg & 4) ? f : s.yci[py[u]]) : -1;
-                }
+                issue(f0, ee, k);
 #pragma unroll
                 for (int u = 0; u < DT_U; u++) {
                     const int f = f0 + u * 64 + lane;
-                    const uint32_t h = dt_hash(k[u]);
+                    const uint32_t h = dt_hash((dbg & 4) ? f : k[u]);
                     const bool c = !(dbg & 2) && f < fu1 && ((filt[h >> 5] >> (h & 31)) & 1u);
                     const unsigned long long m = __ballot(c);
                     if (c) stg[cnt + __popcll(m & ltmask)] = f | (ee[u] << 17);
@@ -678,7 +691,12 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
     int cap = DT_CAP;
     int64_t win = DT_WIN;
     if (gb_knob("dot_cap") > DT_MID && gb_knob("dot_cap") < DT_CAP) cap = (int)gb_knob("dot_cap");
-    if (gb_knob("dot_win") >= DT_OVH && gb_knob("dot_win") < DT_WIN) win = gb_knob("dot_win");
+    // per-entry cost of the task cut (knob dot_ovh, >= DT_OVH_MIN): at most win / ovh entries per task
+    // tools/spgemm_probe.py (R-MAT, one box): ovh 256 -> 128 (up to 256 entries per task, so
+    // fewer tasks, X loads and filter builds): s22 118.7 -> 111.3 ms, s20 24.1 -> 23.2 ms
+    int64_t ovh = DT_OVH;
+    if (gb_knob("dot_ovh") >= DT_OVH_MIN) ovh = gb_knob("dot_ovh");
+    if (gb_knob("dot_win") >= ovh && gb_knob("dot_win") < DT_WIN) win = gb_knob("dot_win");
     uint8_t *hflag = s.get<uint8_t>(nm);
     gb_memset(hflag, 0, nm);
     uint8_t *tf = s.get<uint8_t>(nm);
@@ -719,7 +737,7 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
                                  int piece) {
                 gb_scratch ts;
                 int64_t *cum = ts.get<int64_t>(ne + 1);
-                gb_exclusive_scan_i32(eB, DT_OVH, cum, ne);
+                gb_exclusive_scan_i32(eB, (int)ovh, cum, ne);
                 uint8_t *tsf = ts.get<uint8_t>(ne);
                 hipLaunchKernelGGL(k_dt_task_flags, dim3(dt_grid(ne)), dim3(DT_BLOCK), 0, gb_stream(), ne, win, eG,
                                    cum, tsf);

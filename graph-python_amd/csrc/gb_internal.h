@@ -172,6 +172,7 @@ extern std::atomic<bool> g_spec_active;
 extern thread_local int g_spec_hold;
 void gb_spec_resolve(const void *keep);
 extern std::atomic<int64_t> g_stat_spec_adopted, g_stat_spec_rollbacks;  // GxB_Global_get_int("stat_...")
+extern std::atomic<int64_t> g_stat_nvals_copy;
 struct gb_spec_hold_guard {
     gb_spec_hold_guard() { g_spec_hold++; }
     ~gb_spec_hold_guard() { g_spec_hold--; }
@@ -246,7 +247,10 @@ uint64_t gb_next_pub_seq();
 // while no later work has been enqueued)
 uint64_t gb_epoch();
 hipStream_t gb_stream_peek();  // the library stream, without counting an enqueue
-// wait for slot->seq == seq; false if the stream drained without it (caller falls back)
+// wait for slot->seq == seq; false if the stream drained without it (caller falls back).
+// A publisher may instead store one tagged word into seq: bit 63 | (seq & 0x7fffffff) << 32 |
+// the 32-bit count (GB_PUB_TAG; a plain seq never has bit 63 set)
+#define GB_PUB_TAG (1ULL << 63)
 bool gb_host_slot_wait(gb_host_slot *s, uint64_t seq, int64_t *value);
 // zero nw bitmap words and (if given) the count, in one launch
 void gb_zero_bitmap(uint64_t *bits, int64_t nw, int64_t *d_count);
@@ -480,6 +484,9 @@ struct gb_asg {
     int q_iso_code = -1;
     int64_t *count = nullptr;  // w's device count
     int64_t h_count = -1;      // w's count before the assign, when the host knew it (-1: not known)
+    // u's device count is exact (written by the kernel that produced u, earlier on the stream):
+    // an empty u ends the launch early (the speculated level after a BFS's last one)
+    bool u_count_exact = false;
 };
 void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, gb_bitmap_view &u,
              const gb_vmask &mask, GrB_Semiring sr, bool flip, const gb_asg *asg = nullptr);

@@ -198,15 +198,36 @@ __device__ __forceinline__ long long gb_push_targets(const int32_t (&j)[4], bool
                                                      const uint64_t *__restrict__ mbits, bool mcomp,
                                                      unsigned long long *__restrict__ tbits,
                                                      const int64_t *__restrict__ hprow, long long &mfn,
-                                                     const uint64_t *__restrict__ qbits) {
-    if (mbits) {
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-            if (ok[u]) ok[u] = (gb_bit(mbits, j[u]) || (qbits && gb_bit(qbits, j[u]))) != mcomp;
-    }
+                                                     const uint64_t *__restrict__ qbits, bool serial = false) {
     unsigned long long cur[4];
+    if (serial) {  // diagnostics (iso_dbg 128): the round-4 order, each read behind the one before
+        if (mbits) {
 #pragma unroll
-    for (int u = 0; u < 4; u++) cur[u] = ok[u] ? tbits[j[u] >> 6] : ~0ULL;
+            for (int u = 0; u < 4; u++)
+                if (ok[u]) ok[u] = (gb_bit(mbits, j[u]) || (qbits && gb_bit(qbits, j[u]))) != mcomp;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) cur[u] = ok[u] ? tbits[j[u] >> 6] : ~0ULL;
+    } else {
+        // the mask words (w's and the fused stamp's q) and the output word of every target
+        // are read at once: one round trip instead of three dependent ones
+        uint64_t mw[4], qw[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            mw[u] = qw[u] = 0;
+            cur[u] = ~0ULL;
+            if (ok[u]) {
+                if (mbits) mw[u] = mbits[j[u] >> 6];
+                if (mbits && qbits) qw[u] = qbits[j[u] >> 6];
+                cur[u] = tbits[j[u] >> 6];
+            }
+        }
+        if (mbits) {
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (ok[u]) ok[u] = ((((mw[u] | qw[u]) >> (j[u] & 63)) & 1ULL) != 0) != mcomp;
+        }
+    }
     long long added = 0;
 #pragma unroll
     for (int u = 0; u < 4; u++) {
@@ -298,12 +319,13 @@ __device__ __forceinline__ void gb_store_sized(void *base, int64_t i, int size, 
     default: ((unsigned long long *)base)[i] = x; break;
     }
 }
+// cpre: w's word already read by the caller (nullptr: read it here)
 __device__ __forceinline__ long long gb_asg_words(const gb_asg_dev &g, int64_t w0, int64_t nwords, uint64_t qw,
-                                                 int lane) {
+                                                 int lane, const uint64_t *cpre = nullptr) {
     long long added = 0;
     const int64_t wl = w0 + (lane & 3);
     if (lane < 4 && wl < nwords && qw) {
-        const uint64_t c = g.bits[wl], nwd = c | qw;
+        const uint64_t c = cpre ? *cpre : g.bits[wl], nwd = c | qw;
         if (nwd != c) g.bits[wl] = nwd;
         added = (long long)__popcll(nwd) - (long long)__popcll(c);
     }
@@ -327,7 +349,7 @@ __device__ __forceinline__ long long gb_push_phase(int64_t nwords_u, const uint6
                                                   unsigned long long *__restrict__ tbits, gb_wlist &L,
                                                   const int64_t *__restrict__ hprow, long long &mfn,
                                                   const uint64_t *__restrict__ qbits, const gb_asg_dev &g,
-                                                  long long &adelta) {
+                                                  long long &adelta, bool serial = false) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -360,7 +382,7 @@ __device__ __forceinline__ long long gb_push_phase(int64_t nwords_u, const uint6
                     ok[u] = p + 64 * u < p1;
                     j[u] = ok[u] ? pcol[p + 64 * u] : 0;
                 }
-                added += gb_push_targets(j, ok, mbits, mcomp, tbits, hprow, mfn, qbits);
+                added += gb_push_targets(j, ok, mbits, mcomp, tbits, hprow, mfn, qbits, serial);
             }
         }
     }
@@ -409,7 +431,7 @@ __device__ __forceinline__ long long gb_push_phase(int64_t nwords_u, const uint6
                     j[u] = pcol[L.p[s] + (e - gb_wlist_start(L, s))];
                 }
             }
-            added += gb_push_targets(j, ok, mbits, mcomp, tbits, hprow, mfn, qbits);
+            added += gb_push_targets(j, ok, mbits, mcomp, tbits, hprow, mfn, qbits, serial);
         }
         gb_wave_sync();
     }
@@ -443,15 +465,20 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
     long long cnt = 0;
     for (int64_t w0 = wave * PULL_U; w0 < nwords; w0 += nwaves * PULL_U) {
         const int64_t wl = w0 + (lane & (PULL_U - 1));
+        const bool inr = wl < nwords;
+        // the step's words read together (the stamp's q, the mask, the rows with entries): the
+        // stamp's store no longer orders the mask read behind it
+        const uint64_t qw = (qbits && inr) ? qbits[wl] : 0;
+        const uint64_t mw = (mbits && inr) ? mbits[wl] : 0;
+        const uint64_t rw = (rne && inr) ? rne[wl] : ~0ULL;
         uint64_t mine = ~0ULL;
         if (qbits) {  // fused assign: w |= q; the mask is w's structure after it
-            const uint64_t qw = wl < nwords ? qbits[wl] : 0;
-            adelta += gb_asg_words(g, w0, nwords, qw, lane);
-            if (mbits) mine = wl < nwords ? (mcomp ? ~(mbits[wl] | qw) : (mbits[wl] | qw)) : 0;
+            adelta += gb_asg_words(g, w0, nwords, qw, lane, g.bits == mbits ? &mw : nullptr);
+            if (mbits) mine = inr ? (mcomp ? ~(mw | qw) : (mw | qw)) : 0;
         } else if (mbits) {
-            mine = wl < nwords ? (mcomp ? ~mbits[wl] : mbits[wl]) : 0;
+            mine = inr ? (mcomp ? ~mw : mw) : 0;
         }
-        if (rne && wl < nwords) mine &= rne[wl];  // rows without entries produce nothing
+        if (rne && inr) mine &= rw;  // rows without entries produce nothing
         if (wl == nwords - 1) mine &= tail;
         if (wl >= nwords) mine = 0;
         if (!__ballot(mine != 0)) {  // nothing open in these words
@@ -477,12 +504,43 @@ __device__ __forceinline__ long long gb_pull_iso_phase(int64_t nrows, const int6
                 hv[u] = make_int4(-1, -1, -1, -1);
                 if (live[u]) hv[u] = reinterpret_cast<const int4 *>(ph)[((w0 + u) << 6) + lane];
             }
+            if (dbg & 128) {  // diagnostics: the round-4 short-circuit probes (A/B)
 #pragma unroll
-            for (int u = 0; u < PULL_U; u++)
-                found[u] = (hv[u].x >= 0 && gb_bit(ubits, hv[u].x)) ||
-                           (hv[u].y >= 0 && gb_bit(ubits, hv[u].y)) ||
-                           (hv[u].z >= 0 && gb_bit(ubits, hv[u].z)) ||
-                           (hv[u].w >= 0 && gb_bit(ubits, hv[u].w));
+                for (int u = 0; u < PULL_U; u++)
+                    found[u] = (hv[u].x >= 0 && gb_bit(ubits, hv[u].x)) ||
+                               (hv[u].y >= 0 && gb_bit(ubits, hv[u].y)) ||
+                               (hv[u].z >= 0 && gb_bit(ubits, hv[u].z)) ||
+                               (hv[u].w >= 0 && gb_bit(ubits, hv[u].w));
+            } else {
+                // the probes in two rounds, each with every load in flight at once: the first
+                // head of every open row, then the other three for the rows it missed (a
+                // short-circuit test makes each probe wait for the one before it: up to 16
+                // dependent frontier reads per wave step)
+                const uint32_t *ub32 = reinterpret_cast<const uint32_t *>(ubits);
+                uint32_t w1[PULL_U];
+#pragma unroll
+                for (int u = 0; u < PULL_U; u++) {
+                    w1[u] = 0;
+                    if (hv[u].x >= 0) w1[u] = ub32[hv[u].x >> 5];
+                }
+#pragma unroll
+                for (int u = 0; u < PULL_U; u++) found[u] = hv[u].x >= 0 && ((w1[u] >> (hv[u].x & 31)) & 1u);
+                uint32_t wy[PULL_U], wz[PULL_U], ww[PULL_U];
+#pragma unroll
+                for (int u = 0; u < PULL_U; u++) {
+                    wy[u] = wz[u] = ww[u] = 0;
+                    if (!found[u]) {
+                        if (hv[u].y >= 0) wy[u] = ub32[hv[u].y >> 5];
+                        if (hv[u].z >= 0) wz[u] = ub32[hv[u].z >> 5];
+                        if (hv[u].w >= 0) ww[u] = ub32[hv[u].w >> 5];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < PULL_U; u++)
+                    found[u] = found[u] || (hv[u].y >= 0 && ((wy[u] >> (hv[u].y & 31)) & 1u)) ||
+                               (hv[u].z >= 0 && ((wz[u] >> (hv[u].z & 31)) & 1u)) ||
+                               (hv[u].w >= 0 && ((ww[u] >> (hv[u].w & 31)) & 1u));
+            }
 #pragma unroll
             for (int u = 0; u < PULL_U; u++) {
                 const int64_t r = ((w0 + u) << 6) + lane;
@@ -676,16 +734,22 @@ struct gb_iso_args {
     bool flip;
     const void *a0, *u0;
     void *iso_out;
-    // host mailbox for the count
+    // host mailbox for the count; pub_form (knob iso_pub): 0 one tagged word (GB_PUB_TAG) stored
+    // relaxed, 1 value + system fence + release seq (round 4), 2 the tagged word stored release
     gb_host_slot *pub;
     long long pub_seq;
+    int pub_form;
+    // u's exact device count (gb_asg::u_count_exact; nullptr: not known): 0 ends the launch early
+    const int64_t *u_exit;
+    bool out_zeroed;  // T's bitmap came zeroed (the spare)
     // a bitmap to zero for the next call's push output
     uint64_t *spare;
     int64_t spare_words;
     // pull shape: lane-per-row steps of 4 edges, then the first per-row cap of the list rounds
     int p1_steps, cap0;
     int dbg;                        // diagnostics (knob iso_dbg): 1 no mailbox, 2 no hint sum, 4 no work, 8 empty,
-                                    // 16 pull without its segment list, 32 pull steps without probes (wrong results)
+                                    // 16 pull without its segment list, 32 pull steps without probes (wrong results),
+                                    // 64 no finish, 128 the round-4 dependent read order (exact; A/B)
     bool packed;                    // one-round finish (iso_finish_packed): n < 2^27
     const uint64_t *rows_nonempty;  // pull rows with entries (nullptr: all)
     const int32_t *phead;           // pull head per row, 4 int32 (nullptr: none; gb_view_pullfirst)
@@ -1114,6 +1178,21 @@ __global__ void k_spmv_fold(SR sr, const int32_t *__restrict__ chunks, int64_t n
 // three separate grid sums: ~5 us per BFS level).
 #define ISO_ARR_BITS 10
 #define ISO_VAL_BITS 27
+
+// hand the count to the host without a copy (gb_host_slot_wait)
+__device__ __forceinline__ void iso_publish(const gb_iso_args &a, long long tot) {
+    if (!a.pub || (a.dbg & 1)) return;
+    if (a.pub_form == 1) {
+        __hip_atomic_store(&a.pub->value, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+        __hip_atomic_store(&a.pub->seq, a.pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    const long long w = (long long)(GB_PUB_TAG | (((unsigned long long)a.pub_seq & 0x7fffffffULL) << 32) |
+                                    ((unsigned long long)tot & 0xffffffffULL));
+    if (a.pub_form == 0) __hip_atomic_store(&a.pub->seq, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else __hip_atomic_store(&a.pub->seq, w, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ void iso_finish_packed(long long cnt, long long mfn, long long adelta,
                                                   unsigned long long *__restrict__ tcount,
                                                   unsigned long long *__restrict__ gst, const gb_iso_args &a) {
@@ -1168,11 +1247,7 @@ __device__ __forceinline__ void iso_finish_packed(long long cnt, long long mfn, 
     const long long tot = (long long)(((o2 >> ISO_ARR_BITS) & VM) + scnt);
     const long long add = (long long)((o2 >> (ISO_ARR_BITS + ISO_VAL_BITS)) + sadd);
     *tcount = (unsigned long long)tot;
-    if (a.pub && !(a.dbg & 1)) {  // hand the count to the host without a copy (gb_host_slot_wait)
-        __hip_atomic_store(&a.pub->value, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __threadfence_system();
-        __hip_atomic_store(&a.pub->seq, a.pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    iso_publish(a, tot);
     // after the publish (off the host's critical path; the next launch on the stream starts
     // only after this kernel has ended): the root reset and the fused assign's count
     atomicExch(root, 0ULL);
@@ -1214,6 +1289,24 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
     // the result's iso value does not depend on the work: evaluated here, off the finish's path
     if (a.packed && a.iso_out && blockIdx.x == 0 && threadIdx.x == 0)
         gb_iso_eval(a.mul, a.xcode, a.zcode, a.flip, a.a0, a.u0, a.iso_out);
+    if (a.u_exit && *a.u_exit == 0) {
+        // an empty u (the speculated level after a BFS's last): no products, an empty stamp, so
+        // no grid-wide finish -- block 0 stores the zero count and hint and publishes
+        if (!a.out_zeroed)
+            for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < ((nrows + 63) >> 6);
+                 w += (int64_t)gridDim.x * blockDim.x)
+                tbits[w] = 0;
+        if (blockIdx.x == 0) {
+            if (a.mf_out)
+                for (int i = threadIdx.x; i < GB_HINT_PARTS; i += blockDim.x) a.mf_out[i] = 0;
+            if (threadIdx.x == 0) {
+                *tcount = 0ULL;
+                if (!a.packed && a.iso_out) gb_iso_eval(a.mul, a.xcode, a.zcode, a.flip, a.a0, a.u0, a.iso_out);
+                iso_publish(a, 0);
+            }
+        }
+        return;
+    }
     // fused assign: q's value mask is empty when q is iso with a false value
     const uint64_t *qbits = nullptr;
     if (a.asg.bits && (!a.asg_qiso || gb_dyn_nonzero(a.asg_qiso, a.asg_qiso_code))) qbits = ubits;
@@ -1222,7 +1315,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
         ;
     else if (push)
         cnt = gb_push_phase(nwords_u, ubits, prow, pcol, hubs, nhubs, H, mbits, mcomp,
-                            (unsigned long long *)tbits, L, a.hprow, mfn, qbits, a.asg, adelta);
+                            (unsigned long long *)tbits, L, a.hprow, mfn, qbits, a.asg, adelta, (a.dbg & 128) != 0);
     else
         cnt = gb_pull_iso_phase(nrows, rowptr, colidx, ubits, mbits, mcomp, tbits, L, a.hprow, mfn, a.p1_steps,
                                 a.cap0, a.rows_nonempty, qbits, a.asg, adelta, a.dbg,
@@ -1236,11 +1329,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
     if (gb_grid_sum(cnt, gst, &tot)) {
         *tcount = (unsigned long long)tot;
         if (a.iso_out) gb_iso_eval(a.mul, a.xcode, a.zcode, a.flip, a.a0, a.u0, a.iso_out);
-        if (a.pub && !(a.dbg & 1)) {  // hand the count to the host without a copy (gb_host_slot_wait)
-            __hip_atomic_store(&a.pub->value, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __threadfence_system();
-            __hip_atomic_store(&a.pub->seq, a.pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        iso_publish(a, tot);
     }
     if (a.mf_out && !(a.dbg & 2)) {
         long long m;
@@ -1571,6 +1660,12 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             }
             args.pub = T.pub ? gb_host_slot_device(T.pub) : nullptr;
             args.pub_seq = (long long)T.pub_seq;
+            // the count travels in one tagged word stored without a fence: the host needs only the
+            // count, and the kernel's end orders everything else for the next launch.  With the
+            // BFS speculation on, tools/ab_bfs.py (s22, 8 interleaved rounds): 0.2298 ms per BFS
+            // vs 0.2325 with value + system fence + release seq (round 3 had measured the reverse
+            // without speculation, when the host waited on every mailbox)
+            args.pub_form = n < (1LL << 31) ? (int)std::max<int64_t>(0, std::min<int64_t>(2, gb_knob("iso_pub"))) : 1;
             // a zeroed output bitmap left by the previous call (push may write into it directly)
             bool spare_taken = false;
             if (g_spare && g_spare_words == nw) {
@@ -1582,6 +1677,8 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             }
             g_spare = nullptr;
             g_spare_words = 0;
+            args.out_zeroed = spare_taken;
+            if (asg && asg->u_count_exact && u.count && gb_knob("spec_empty_exit") != 1) args.u_exit = u.count;
             bool need_prep = false;
             if (can_push) {
                 units = std::max<int64_t>(units, std::max<int64_t>((Apush->nhubs + 15) / 16, (uw + 3) / 4));

@@ -159,6 +159,8 @@ void gb_obj_free_storage(GB_Obj *A) {
     A->dense = nullptr;
 }
 
+std::atomic<int64_t> g_stat_nvals_copy{0};
+
 int64_t gb_nvals(GB_Obj *A) {
     if (A->kind == GB_KIND_MATRIX && !A->cw) return A->nvals;
     if (!A->nvals_valid) {
@@ -166,6 +168,7 @@ int64_t gb_nvals(GB_Obj *A) {
         if (A->pub && A->pub_seq && A->pub_epoch == gb_epoch() && gb_host_slot_wait(A->pub, A->pub_seq, &v)) {
             A->nvals = v;  // published by the kernel that produced d_nvals
         } else {
+            g_stat_nvals_copy.fetch_add(1, std::memory_order_relaxed);
             A->nvals = gb_read_i64(A->cw ? A->cw_stat : A->d_nvals);
         }
         A->nvals_valid = true;

@@ -821,6 +821,7 @@ static void spec_launch_locked(GB_Obj *q, GB_Obj *v, GB_Obj *A, GrB_Semiring sr,
     asg.q_iso_code = q->type->code;
     asg.count = v->d_nvals;
     asg.h_count = -1;
+    asg.u_count_exact = true;  // q was just produced by the kernel before this one
     spmv_views V;
     spmv_build_views(V, v, sr, A, q, d, vxm, q->nrows, &asg);
     if (!V.iso_result) return;
@@ -856,7 +857,7 @@ static bool same_desc(const gb_desc &a, const gb_desc &b) {
 // notebook loop's shape
 static void spec_after_level(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr, GB_Obj *A, GB_Obj *u,
                              const gb_desc &d, bool vxm, const gb_asg &asg, bool direct, bool published) {
-    if (gb_knob("bfs_spec") == 1 || gb_knob("iso_dbg") != 0) return;
+    if (gb_knob("bfs_spec") == 1 || (gb_knob("iso_dbg") & ~128) != 0) return;  // 128: an A/B order, exact
     if (!direct || !published || accum || w != u || !mask || !d.replace || !d.comp || !d.structure) return;
     if (w->kind == GB_KIND_MATRIX || mask->kind == GB_KIND_MATRIX || A->kind != GB_KIND_MATRIX || A->cw) return;
     if (!spec_int_type(mask->type->code) || asg.bits != mask->bits || asg.vals != mask->dense) return;

@@ -61,7 +61,7 @@ def read_vec(lib, v, n):
     return out, nv.value
 
 
-def ref_loop(G, src, stamps, mxv=False):
+def ref_loop(G, src, stamps, mxv=False, stop=True):
     """numpy restatement: for level k the stamp value stamps[k] (None: no stamp that level);
     v<q> = s; q<!v.S, replace> = q (any.pair) A  (vxm: successors; mxv on A: predecessors)"""
     n = G.nrows
@@ -80,13 +80,15 @@ def ref_loop(G, src, stamps, mxv=False):
         else:    # w(j) = OR_i q(i) A(i,j)
             nxt[G.indices[q[rows]]] = True
         q = nxt & ~have
-        if not q.any():
+        if stop and not q.any():
             break
     return v, q
 
 
-def run_loop(gb, A, n, src, stamps, sr_name="any_pair", mxv=False, stamp_desc=None, hooks=None):
-    """the loop through the C ABI; hooks[k](q, v) runs after level k's nvals"""
+def run_loop(gb, A, n, src, stamps, sr_name="any_pair", mxv=False, stamp_desc=None, hooks=None, stop=True,
+             counts=None):
+    """the loop through the C ABI; hooks[k](q, v) runs after level k's nvals; stop=False keeps
+    going after an empty frontier; counts collects each level's nvals(q)"""
     lib = gb.lib
     sr = lib.GxB_ANY_PAIR_BOOL if sr_name == "any_pair" else lib.GrB_LOR_LAND_SEMIRING_BOOL
     q, v = ctypes.c_void_p(), ctypes.c_void_p()
@@ -102,9 +104,11 @@ def run_loop(gb, A, n, src, stamps, sr_name="any_pair", mxv=False, stamp_desc=No
         else:
             ok(lib.GrB_vxm(q, v, None, sr, q, A._carg, lib.GrB_DESC_RSC), "vxm")
         ok(lib.GrB_Vector_nvals(ctypes.byref(nv), q), "nvals q")
+        if counts is not None:
+            counts.append(nv.value)
         if hooks and k in hooks:
             hooks[k](q, v)
-        if nv.value == 0:
+        if stop and nv.value == 0:
             break
     got, cnt = read_vec(lib, v, n)
     qb, _ = read_vec_bool(lib, q, n)
@@ -160,6 +164,32 @@ def test_spec_off_gives_the_same(gb, graph):
     finally:
         gb.set_knob("bfs_spec", 0)
     assert np.array_equal(on, off)
+
+
+def test_spec_past_the_empty_level(gb, graph):
+    """levels issued after the frontier emptied: the speculated level on an empty q ends its
+    launch early (a zero count, an empty result, no stamp); adopting it must look like a full
+    level -- v unchanged, q empty, every count 0 -- and a loop that then stamps v again agrees"""
+    G, A = graph
+    n = G.nrows
+    src = roots(G)[0]
+    ref, _ = ref_loop(G, src, list(range(1, 64)))
+    depth = int(ref.max())
+    stamps = list(range(1, depth + 5))
+    a0 = stat(gb, "stat_bfs_spec_adopted")
+    counts = []
+    got, q = run_loop(gb, A, n, src, stamps, stop=False, counts=counts)
+    exp, eq = ref_loop(G, src, stamps, stop=False)
+    assert np.array_equal(got, exp) and np.array_equal(q, eq) and not q.any()
+    assert counts[depth - 1:] == [0] * (len(stamps) - depth + 1), counts
+    assert stat(gb, "stat_bfs_spec_adopted") >= a0 + len(stamps) - 2
+    gb.set_knob("spec_empty_exit", 1)  # the same loop with full launches on the empty levels
+    try:
+        counts_full = []
+        full, _ = run_loop(gb, A, n, src, stamps, stop=False, counts=counts_full)
+    finally:
+        gb.set_knob("spec_empty_exit", 0)
+    assert np.array_equal(full, got) and counts_full == counts
 
 
 def test_spec_unexpected_stamps(gb, graph):
