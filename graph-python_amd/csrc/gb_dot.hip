@@ -155,21 +155,27 @@ __global__ void k_dt_piece_flags(dt_side s, int64_t nh, int piece, int cap, cons
     }
 }
 
-__global__ void k_dt_piece_compact(int64_t nh, int cap, const uint8_t *__restrict__ cnt,
+// all pieces at once: pair q = j * nh + i (piece-major, so a group's entries of one piece are
+// consecutive and its tasks share that piece's keys); ePc[e] = the piece
+__global__ void k_dt_piece_compact(int64_t nh, int64_t npairs, int cap, const uint8_t *__restrict__ cnt,
                                    const int64_t *__restrict__ pos, const int32_t *__restrict__ hG,
                                    const int32_t *__restrict__ hO, const int64_t *__restrict__ hQ,
                                    const int64_t *__restrict__ pys, const int32_t *__restrict__ pb,
                                    int32_t *__restrict__ eG, int64_t *__restrict__ eYS, int32_t *__restrict__ eO,
-                                   int32_t *__restrict__ eB, int64_t *__restrict__ eQ) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nh; i += (int64_t)gridDim.x * blockDim.x) {
-        for (int c = 0; c < cnt[i]; c++) {
-            const int64_t e = pos[i] + c;
+                                   int32_t *__restrict__ eB, int64_t *__restrict__ eQ, uint16_t *__restrict__ ePc) {
+    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < npairs;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = q % nh;
+        const uint16_t j = (uint16_t)(q / nh);
+        for (int c = 0; c < cnt[q]; c++) {
+            const int64_t e = pos[q] + c;
             const int64_t o0 = (int64_t)c * cap;
             eG[e] = hG[i];
-            eYS[e] = pys[i] + o0;
+            eYS[e] = pys[q] + o0;
             eO[e] = hO[i];
-            eB[e] = (int32_t)(pb[i] - o0 < cap ? pb[i] - o0 : cap);
+            eB[e] = (int32_t)(pb[q] - o0 < cap ? pb[q] - o0 : cap);
             eQ[e] = hQ[i];
+            ePc[e] = j;
         }
     }
 }
@@ -190,9 +196,11 @@ __global__ void k_dt_ident(int64_t nh, const int64_t *__restrict__ hQ, Z *__rest
 
 // a task starts where the group changes or the cost prefix enters a new window
 __global__ void k_dt_task_flags(int64_t ne, int64_t win, const int32_t *__restrict__ eG,
-                                const int64_t *__restrict__ cum, uint8_t *__restrict__ ts) {
+                                const uint16_t *__restrict__ ePc, const int64_t *__restrict__ cum,
+                                uint8_t *__restrict__ ts) {
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x)
-        ts[e] = (e == 0 || eG[e] != eG[e - 1] || cum[e] / win != cum[e - 1] / win) ? 1 : 0;
+        ts[e] = (e == 0 || eG[e] != eG[e - 1] || (ePc && ePc[e] != ePc[e - 1]) || cum[e] / win != cum[e - 1] / win)
+                    ? 1 : 0;
 }
 
 __global__ void k_dt_task_fill(int64_t ne, const uint8_t *__restrict__ ts, const int64_t *__restrict__ tpos,
@@ -435,8 +443,8 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
     SR sr, int mon, dt_side s, const X *__restrict__ xvx, bool x_iso, const X *__restrict__ yvx, bool y_iso,
     int64_t ntask, const int64_t *__restrict__ tstart, const int32_t *__restrict__ eG,
     const int64_t *__restrict__ eYS, const int32_t *__restrict__ eO, const int32_t *__restrict__ eB,
-    const int64_t *__restrict__ eQ, Z *__restrict__ tval, uint8_t *__restrict__ tflag, int dbg, int piece,
-    int pcap, unsigned long long *__restrict__ tctr, int chunk) {
+    const int64_t *__restrict__ eQ, Z *__restrict__ tval, uint8_t *__restrict__ tflag, int dbg,
+    const uint16_t *__restrict__ ePc, int pcap, unsigned long long *__restrict__ tctr, int chunk) {
     __shared__ int32_t keys[DT_CAP];
     __shared__ uint32_t filt[1 << (DT_FLOG - 5)];
     __shared__ uint64_t estart[DT_SMAX / 64 + 1];     // bit f: an entry starts at flat element f
@@ -462,6 +470,7 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
     // whose keys and filter then stay in LDS
     __shared__ int64_t s_chunk;
     int64_t prev_g = -1;
+    int prev_pc = -1;
     for (;;) {
     if (tid == 0) s_chunk = (int64_t)atomicAdd(tctr, (unsigned long long)chunk);
     __syncthreads();
@@ -473,11 +482,13 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
         const int64_t e0 = tstart[t];
         const int ne = __builtin_amdgcn_readfirstlane((int)(tstart[t + 1] - e0));
         const int64_t g = eG[e0];
-        const bool reuse = g == prev_g && !(dbg & 64);  // dbg 64: reload X every task (A/B)
+        const int piece = ePc ? (int)ePc[e0] : -1;  // a piece of a list longer than the cap
+        const bool reuse = g == prev_g && piece == prev_pc && !(dbg & 64);  // dbg 64: reload X every task (A/B)
         prev_g = g;
+        prev_pc = piece;
         int64_t xs = s.xrp[g];
         int64_t alen = s.xrp[g + 1] - xs;
-        if (piece >= 0) {  // piece `piece` of a list longer than the cap
+        if (piece >= 0) {
             xs += (int64_t)piece * pcap;
             alen -= (int64_t)piece * pcap;
             if (alen > pcap) alen = pcap;
@@ -734,13 +745,13 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
             GB_LAUNCH_CHECK();
             // tasks over (eG, eYS, eO, eB, eQ) in task order: cut at group changes and windows
             auto run_tasks = [&](int64_t ne, int32_t *eG, int64_t *eYS, int32_t *eO, int32_t *eB, int64_t *eQ,
-                                 int piece) {
+                                 const uint16_t *ePc) {
                 gb_scratch ts;
                 int64_t *cum = ts.get<int64_t>(ne + 1);
                 gb_exclusive_scan_i32(eB, (int)ovh, cum, ne);
                 uint8_t *tsf = ts.get<uint8_t>(ne);
                 hipLaunchKernelGGL(k_dt_task_flags, dim3(dt_grid(ne)), dim3(DT_BLOCK), 0, gb_stream(), ne, win, eG,
-                                   cum, tsf);
+                                   ePc, cum, tsf);
                 int64_t *tpos = ts.get<int64_t>(ne + 1);
                 gb_exclusive_scan_u8(tsf, tpos, ne);
                 const int64_t nt = gb_read_i64(tpos + ne);
@@ -759,7 +770,7 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
                 if (!(skip & 2))
                     hipLaunchKernelGGL((k_dot_task<SRT, X, Z, SWAP>), dim3(gt), dim3(DT_TB), 0, gb_stream(), srf,
                                        info.mon, sd, xv, xiso, yv, yiso, nt, tstart, eG, eYS, eO, eB, eQ, (Z *)tval,
-                                       tflag, (int)gb_knob("dot_dbg"), piece, cap, tctr, (int)chunk);
+                                       tflag, (int)gb_knob("dot_dbg"), ePc, cap, tctr, (int)chunk);
                 GB_LAUNCH_CHECK();
             };
             gb_exclusive_scan_u8(tf, pos, nm);
@@ -774,7 +785,7 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
                 hipLaunchKernelGGL((k_dt_compact<SWAP>), dim3(gw), dim3(DT_BLOCK), 0, gb_stream(), sd, cap, tf, pos,
                                    eG, eYS, eO, eB, eQ, false, nullptr);
                 GB_LAUNCH_CHECK();
-                run_tasks(ne, eG, eYS, eO, eB, eQ, -1);
+                run_tasks(ne, eG, eYS, eO, eB, eQ, nullptr);
             }
             if (!pieces) return;
             gb_exclusive_scan_u8(hg, pos, nm);
@@ -810,28 +821,31 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
             GB_LAUNCH_CHECK();
             const int64_t amx = gb_read_i64((const int64_t *)amax);
             const int np = (int)((amx + cap - 1) / cap);
-            uint8_t *pc = hs.get<uint8_t>(nh);
-            int64_t *ppos = hs.get<int64_t>(nh + 1);
-            int64_t *pys = hs.get<int64_t>(nh);
-            int32_t *pb = hs.get<int32_t>(nh);
-            for (int j = 0; j < np; j++) {
+            // every piece's runs at once (pairs piece-major): one scan, one compaction, one task
+            // launch (round 4: one pass per piece, each ending on a host read of its size)
+            const int64_t npairs = nh * (int64_t)np;
+            uint8_t *pc = hs.get<uint8_t>(npairs);
+            int64_t *ppos = hs.get<int64_t>(npairs + 1);
+            int64_t *pys = hs.get<int64_t>(npairs);
+            int32_t *pb = hs.get<int32_t>(npairs);
+            for (int j = 0; j < np; j++)
                 hipLaunchKernelGGL(k_dt_piece_flags, dim3(dt_grid(nh)), dim3(DT_BLOCK), 0, gb_stream(), sd, nh, j,
-                                   cap, hG, hYS, hB, pc, pys, pb);
-                GB_LAUNCH_CHECK();
-                gb_exclusive_scan_u8(pc, ppos, nh);
-                const int64_t npe = gb_read_i64(ppos + nh);
-                if (npe == 0) continue;
-                gb_scratch ps;
-                int32_t *eG = ps.get<int32_t>(npe);
-                int64_t *eYS = ps.get<int64_t>(npe);
-                int32_t *eO = ps.get<int32_t>(npe);
-                int32_t *eB = ps.get<int32_t>(npe);
-                int64_t *eQ = ps.get<int64_t>(npe);
-                hipLaunchKernelGGL(k_dt_piece_compact, dim3(dt_grid(nh)), dim3(DT_BLOCK), 0, gb_stream(), nh, cap, pc,
-                                   ppos, hG, hO, hQ, pys, pb, eG, eYS, eO, eB, eQ);
-                GB_LAUNCH_CHECK();
-                run_tasks(npe, eG, eYS, eO, eB, eQ, j);
-            }
+                                   cap, hG, hYS, hB, pc + j * nh, pys + j * nh, pb + j * nh);
+            GB_LAUNCH_CHECK();
+            gb_exclusive_scan_u8(pc, ppos, npairs);
+            const int64_t npe = gb_read_i64(ppos + npairs);
+            if (npe == 0) return;
+            gb_scratch ps;
+            int32_t *eG = ps.get<int32_t>(npe);
+            int64_t *eYS = ps.get<int64_t>(npe);
+            int32_t *eO = ps.get<int32_t>(npe);
+            int32_t *eB = ps.get<int32_t>(npe);
+            int64_t *eQ = ps.get<int64_t>(npe);
+            uint16_t *ePc = ps.get<uint16_t>(npe);
+            hipLaunchKernelGGL(k_dt_piece_compact, dim3(dt_grid(npairs)), dim3(DT_BLOCK), 0, gb_stream(), nh, npairs,
+                               cap, pc, ppos, hG, hO, hQ, pys, pb, eG, eYS, eO, eB, eQ, ePc);
+            GB_LAUNCH_CHECK();
+            run_tasks(npe, eG, eYS, eO, eB, eQ, ePc);
         };
         phase(std::false_type{});
         phase(std::true_type{});

@@ -1642,8 +1642,10 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             // any_pair: 0.340 ms/BFS without, 0.356 with 2, 0.350 with 1)
             args.p1_steps = (int)gb_knob("pull_steps");
             if (args.p1_steps < 0) args.p1_steps = 0;
+            // first per-row cap of the pull's segment-list rounds: tools/ab_bfs.py (s22, 6 interleaved
+            // rounds, after the two-round head probes): 16 -> 0.2285, 32 -> 0.2266, 64 -> 0.2260 ms/BFS
             args.cap0 = (int)gb_knob("pull_cap");
-            if (args.cap0 <= 0) args.cap0 = 16;
+            if (args.cap0 <= 0) args.cap0 = 64;
             args.rows_nonempty = A.nonempty;
             args.phead = A.phead;
             args.pdeg = A.pdeg;
