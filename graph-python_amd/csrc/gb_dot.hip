@@ -39,8 +39,8 @@ constexpr int DT_BLOCK = 256;
 constexpr int DT_SMALL = 64;      // long side <= 64: k_dot_small, keys one per lane
 constexpr int DT_MID = 256;       // long side <= 256: k_dot_small, four keys per lane
 constexpr int DT_CAP = 8192;      // long side <= DT_CAP: k_dot_task (keys in LDS)
-constexpr int DT_OVH = 128;       // per-entry cost added to the streamed length (task windows)
-constexpr int DT_OVH_MIN = 128;   // the least per-entry cost (knob dot_ovh): sizes the task's entry arrays
+constexpr int DT_OVH = 64;        // per-entry cost added to the streamed length (task windows)
+constexpr int DT_OVH_MIN = 64;    // the least per-entry cost (knob dot_ovh): sizes the task's entry arrays
 constexpr int DT_WIN = 32768;     // task window: <= DT_WIN / ovh entries start in one
 constexpr int DT_MAXE = DT_WIN / DT_OVH_MIN;
 
@@ -450,11 +450,10 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
     __shared__ uint64_t estart[DT_SMAX / 64 + 1];     // bit f: an entry starts at flat element f
     __shared__ int32_t stage[DT_TB / 64][64 * DT_U];  // staged flat element | entry << 17
     __shared__ int64_t e_ys[DT_MAXE];
-    __shared__ int64_t e_q[DT_MAXE];
-    __shared__ int32_t e_o[DT_MAXE];
     __shared__ int32_t e_pre[DT_MAXE + 1];
     __shared__ unsigned long long e_acc[DT_MAXE];
-    __shared__ int e_fnd[DT_MAXE];
+    __shared__ uint32_t e_fnd[DT_MAXE / 32];  // bit e: entry e found a match (the output slot and
+                                              // other index stay in global memory: LDS holds 512 entries)
     __shared__ int w_sum[DT_TB / 64];
     __shared__ int next_unit;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -497,16 +496,14 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
         if (!reuse)
             for (int i = tid; i < (1 << (DT_FLOG - 5)); i += DT_TB) filt[i] = 0;
         for (int i = tid; i < DT_SMAX / 64 + 1; i += DT_TB) estart[i] = 0;
+        for (int i = tid; i < DT_MAXE / 32; i += DT_TB) e_fnd[i] = 0;
         int b = 0;
         if (tid < ne) {
             b = eB[e0 + tid];
             e_ys[tid] = eYS[e0 + tid];
-            e_o[tid] = eO[e0 + tid];
-            e_q[tid] = eQ[e0 + tid];
             unsigned long long iv = 0;
             __builtin_memcpy(&iv, &ident, sizeof(Z));
             e_acc[tid] = iv;
-            e_fnd[tid] = 0;
         }
         int inc = b;
 #pragma unroll
@@ -619,11 +616,11 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
                             xv = xvx[x_iso ? 0 : xs + l];
                             yv = yvx[y_iso ? 0 : p];
                         }
-                        const Z z = dt_mult<SR, X, Z, SWAP>(sr, xv, yv, g, kk, e_o[e]);
+                        const Z z = dt_mult<SR, X, Z, SWAP>(sr, xv, yv, g, kk, eO[e0 + e]);
                         if (e != cur_e) {  // a lane's staged elements come in entry order
                             if (found) {
                                 dt_slot_fold(sr, ANY, &e_acc[cur_e], acc);
-                                e_fnd[cur_e] = 1;
+                                atomicOr(&e_fnd[cur_e >> 5], 1u << (cur_e & 31));
                             }
                             cur_e = e;
                             found = false;
@@ -642,11 +639,11 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
                     dt_wave_fold(sr, found, acc);
                     if (lane == 0) {
                         dt_slot_fold(sr, ANY, &e_acc[e_first], acc);
-                        e_fnd[e_first] = 1;
+                        atomicOr(&e_fnd[e_first >> 5], 1u << (e_first & 31));
                     }
                 } else if (found) {
                     dt_slot_fold(sr, ANY, &e_acc[cur_e], acc);
-                    e_fnd[cur_e] = 1;
+                    atomicOr(&e_fnd[cur_e >> 5], 1u << (cur_e & 31));
                 }
             }
             int nxt = 0;
@@ -654,13 +651,14 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
             unit = __builtin_amdgcn_readlane(nxt, 0);
         }
         __syncthreads();
-        if (tid < ne && e_fnd[tid]) {
+        if (tid < ne && ((e_fnd[tid >> 5] >> (tid & 31)) & 1u)) {
+            const int64_t q = eQ[e0 + tid];
             Z v;
             const unsigned long long raw = e_acc[tid];
             __builtin_memcpy(&v, &raw, sizeof(Z));
-            if (piece >= 0) dt_global_fold(sr, ANY, &tval[e_q[tid]], v);
-            else tval[e_q[tid]] = v;
-            tflag[e_q[tid]] = 1;
+            if (piece >= 0) dt_global_fold(sr, ANY, &tval[q], v);
+            else tval[q] = v;
+            tflag[q] = 1;
         }
         __syncthreads();
     }
@@ -703,8 +701,10 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
     int64_t win = DT_WIN;
     if (gb_knob("dot_cap") > DT_MID && gb_knob("dot_cap") < DT_CAP) cap = (int)gb_knob("dot_cap");
     // per-entry cost of the task cut (knob dot_ovh, >= DT_OVH_MIN): at most win / ovh entries per task
-    // tools/spgemm_probe.py (R-MAT, one box): ovh 256 -> 128 (up to 256 entries per task, so
-    // fewer tasks, X loads and filter builds): s22 118.7 -> 111.3 ms, s20 24.1 -> 23.2 ms
+    // tools/spgemm_probe.py (R-MAT, one box each): ovh 256 -> 128 (up to 256 entries per task, so
+    // fewer tasks, X loads and filter builds): s22 118.7 -> 111.3 ms, s20 24.1 -> 23.2 ms; with the
+    // entry arrays trimmed to fit 512 entries, 128 / 96 / 64: s22 106.2 / 104.2 / 101.7 ms,
+    // s20 21.7 / 21.2 / 20.7 ms
     int64_t ovh = DT_OVH;
     if (gb_knob("dot_ovh") >= DT_OVH_MIN) ovh = gb_knob("dot_ovh");
     if (gb_knob("dot_win") >= ovh && gb_knob("dot_win") < DT_WIN) win = gb_knob("dot_win");
