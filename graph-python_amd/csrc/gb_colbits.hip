@@ -100,6 +100,7 @@ struct cb_step_args {
     const int32_t *p_tab, *s_tab;           // hub pieces (row, piece) of the pull / push orientation
     int64_t p_nhub, s_nhub, H;
     const uint64_t *Fhot;                   // pci relabelled (gb_view_hot): F of the hot sources, rank order
+    bool serial;                            // knob colbits_serial: the round-4 gather order (A/B)
 };
 
 // the level pushes (same rule as k_cw_step)
@@ -188,9 +189,28 @@ GB_DEV void cb_pull_chunk(const cb_step_args &a, int64_t j, bool m_on, bool use_
             const int64_t q = (int64_t)t + cb_shfl_i64(eb, c[u] < 64 ? c[u] : 0);
             src[u] = t < T ? ci[q] : 0;
         }
+        if (a.serial || !use_sum) {
 #pragma unroll
-        for (int u = 0; u < CB_U; u++)
-            if (c[u] < 64) f[u] = cb_gather(a, src[u], use_sum);
+            for (int u = 0; u < CB_U; u++)
+                if (c[u] < 64) f[u] = cb_gather(a, src[u], use_sum);
+        } else {
+            // a sparse frontier: every window's summary word first, then the frontier words of
+            // the sources it marks, each round with all loads in flight (cb_gather's test orders
+            // each window's summary read behind the previous window's word)
+            uint64_t sw[CB_U];
+#pragma unroll
+            for (int u = 0; u < CB_U; u++) {
+                sw[u] = 0;
+                if (c[u] < 64 && src[u] >= 0) sw[u] = a.S_in[src[u] >> 6];
+            }
+#pragma unroll
+            for (int u = 0; u < CB_U; u++) {
+                if (c[u] < 64) {
+                    if (src[u] < 0) f[u] = a.Fhot[src[u] & 0x7fffffff];
+                    else if ((sw[u] >> (src[u] & 63)) & 1ULL) f[u] = a.F[src[u]];
+                }
+            }
+        }
 #pragma unroll
         for (int u = 0; u < CB_U; u++) {
             uint64_t x = f[u];
@@ -858,6 +878,7 @@ bool gb_colbits_mxm(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, GrB_Semiring sr, G
     int64_t alpha = gb_knob("colbits_alpha");
     a.alpha = alpha > 0 ? alpha : 8;
     a.dir = (int)dir;
+    a.serial = gb_knob("colbits_serial") == 1;
     a.stat_out = stat;
     a.gst = grid_state(0);
     a.gst2 = grid_state(1);

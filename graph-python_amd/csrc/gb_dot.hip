@@ -820,10 +820,17 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
                                ident);
             GB_LAUNCH_CHECK();
             const int64_t amx = gb_read_i64((const int64_t *)amax);
-            const int np = (int)((amx + cap - 1) / cap);
+            const int64_t np = (amx + cap - 1) / cap;
+            if (np > 65535) {  // the piece index travels as 16 bits (ePc): such lists (> 2^29 keys)
+                               // go to the per-entry kernel
+                hipLaunchKernelGGL(k_dt_huge_to_csr, dim3(dt_grid(nm)), dim3(DT_BLOCK), 0, gb_stream(), nm, hg,
+                                   sd.perm, hflag);
+                GB_LAUNCH_CHECK();
+                return;
+            }
             // every piece's runs at once (pairs piece-major): one scan, one compaction, one task
             // launch (round 4: one pass per piece, each ending on a host read of its size)
-            const int64_t npairs = nh * (int64_t)np;
+            const int64_t npairs = nh * np;
             uint8_t *pc = hs.get<uint8_t>(npairs);
             int64_t *ppos = hs.get<int64_t>(npairs + 1);
             int64_t *pys = hs.get<int64_t>(npairs);

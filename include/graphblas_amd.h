@@ -436,7 +436,10 @@ GrB_Info GxB_Matrix_prepare_transpose(GrB_Matrix A);
 GrB_Info GxB_MatrixMarket_read_coo(const char *path, GrB_Index *nrows, GrB_Index *ncols, GrB_Index *nvals,
                                    int *type_code, GrB_Index **I, GrB_Index **J, void **X);
 GrB_Info GxB_MatrixMarket_free(void *p);
-/* Backend selection knobs for benchmarking ablations: 0 = automatic. */
+/* Backend selection knobs for benchmarking ablations: 0 = automatic.  get_int also reads
+ * the read-only counters "stat_bfs_spec_adopted" / "stat_bfs_spec_rollbacks" (BFS level
+ * speculation) and "stat_nvals_copy" (vector counts read by a device copy
+ * instead of the producing kernel's host mailbox). */
 GrB_Info GxB_Global_set_int(const char *key, int64_t value);
 GrB_Info GxB_Global_get_int(const char *key, int64_t *value);
 
