@@ -857,7 +857,7 @@ bool gb_colbits_mxm(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, GrB_Semiring sr, G
     gb_view_hubs(pv, B, d.tran1 ? 0 : 1, H);
     if (dir != 1) gb_view_hubs(sv, B, d.tran1 ? 1 : 0, H);
     if (!C->pub) C->pub = gb_host_slot_alloc();
-    const uint64_t seq = gb_next_pub_seq();
+    const uint64_t seq = gb_next_pub_seq(C->pub);
 
     cb_step_args a{};
     a.nout = bc;
@@ -1043,7 +1043,7 @@ GrB_Info GxB_Matrix_colwords_touch(GrB_Matrix A) {
             o->iso = true;
         }
         if (!o->pub) o->pub = gb_host_slot_alloc();
-        const uint64_t seq = gb_next_pub_seq();
+        const uint64_t seq = gb_next_pub_seq(o->pub);
         const int64_t n = o->ncols;
         hipLaunchKernelGGL(k_cw_recount, dim3(cb_grid(n, 2048)), dim3(CB_BLOCK), 0, gb_stream(), o->cw, n, o->cw + n,
                            o->cw_stat, grid_state(0), gb_host_slot_device(o->pub), (long long)seq);

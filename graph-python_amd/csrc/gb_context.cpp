@@ -100,12 +100,16 @@ gb_host_slot *gb_host_slot_alloc() {
     }
     gb_host_slot *s = g_slot_free.back();
     g_slot_free.pop_back();
+    __atomic_store_n(&s->seq, 0LL, __ATOMIC_RELEASE);  // no word of a previous owner can match
+    s->pad[0] = 0;
     return s;
 }
 
 void gb_host_slot_release(gb_host_slot *s) {
     if (!s) return;
     std::lock_guard<std::mutex> lk(g_slot_mu);
+    __atomic_store_n(&s->seq, 0LL, __ATOMIC_RELEASE);
+    s->pad[0] = 0;
     g_slot_free.push_back(s);
 }
 
@@ -116,7 +120,20 @@ gb_host_slot *gb_host_slot_device(gb_host_slot *s) {
     return nullptr;
 }
 
-uint64_t gb_next_pub_seq() { return g_pub_seq.fetch_add(1, std::memory_order_relaxed) + 1; }
+// A tagged one-word publish carries 31 bits of the sequence number, so a word a slot kept
+// from a publish 2^30 or more numbers ago could alias a later one: such a word is cleared before
+// the slot's next publish is issued (that old publish has completed: all library work is on one
+// stream, and 2^30 launches have been issued behind it).  pad[0] holds, on the host only, the
+// last number issued to the slot.
+uint64_t gb_next_pub_seq(gb_host_slot *s) {
+    const uint64_t seq = g_pub_seq.fetch_add(1, std::memory_order_relaxed) + 1;
+    if (s) {
+        const uint64_t last = (uint64_t)s->pad[0];
+        if (last && seq - last >= (1ULL << 30)) __atomic_store_n(&s->seq, 0LL, __ATOMIC_RELEASE);
+        s->pad[0] = (long long)seq;
+    }
+    return seq;
+}
 
 static inline bool slot_match(gb_host_slot *s, uint64_t seq, int64_t *value) {
     const uint64_t w = (uint64_t)__atomic_load_n(&s->seq, __ATOMIC_ACQUIRE);
@@ -445,6 +462,10 @@ GrB_Info GxB_Global_get_int(const char *key, int64_t *value) {
         return GrB_SUCCESS;
     }
     // vector counts read with a device copy (stream sync) instead of the kernel's mailbox
+    if (!strcmp(key, "stat_spmv_host_push")) {
+        *value = g_stat_host_push.load(std::memory_order_relaxed);
+        return GrB_SUCCESS;
+    }
     if (!strcmp(key, "stat_nvals_copy")) {
         *value = g_stat_nvals_copy.load(std::memory_order_relaxed);
         return GrB_SUCCESS;

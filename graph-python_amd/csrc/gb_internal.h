@@ -173,6 +173,7 @@ extern thread_local int g_spec_hold;
 void gb_spec_resolve(const void *keep);
 extern std::atomic<int64_t> g_stat_spec_adopted, g_stat_spec_rollbacks;  // GxB_Global_get_int("stat_...")
 extern std::atomic<int64_t> g_stat_nvals_copy;
+extern std::atomic<int64_t> g_stat_host_push;  // SpMV launches whose push direction the host proved
 struct gb_spec_hold_guard {
     gb_spec_hold_guard() { g_spec_hold++; }
     ~gb_spec_hold_guard() { g_spec_hold--; }
@@ -242,7 +243,7 @@ struct gb_host_slot {
 gb_host_slot *gb_host_slot_alloc();
 void gb_host_slot_release(gb_host_slot *s);
 gb_host_slot *gb_host_slot_device(gb_host_slot *s);  // device address of the same slot
-uint64_t gb_next_pub_seq();
+uint64_t gb_next_pub_seq(gb_host_slot *s);  // the next publish number for slot s
 // count of work enqueued through gb_stream() (a published value is current only
 // while no later work has been enqueued)
 uint64_t gb_epoch();

@@ -1695,6 +1695,12 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
                 bool push_sure = false;
                 if (!hint_ok && spare_taken && eval_ok && u.h_nvals >= 0 && Apush->maxdeg >= 0 &&
                     gb_knob("host_dir") != 1) {
+                    // open rows (where the output may be written) from below.  mask.h_count is the
+                    // mask's set-bit count; do_spmv fills it from a stored-entry count (an upper
+                    // bound on the set bits of a value mask, whose stored entries may be false)
+                    // only for structural or complemented masks, or when the mask is empty -- so
+                    // for a plain value mask it is never an over-estimate (tests/test_gpu_parity.py::
+                    // test_value_mask_false_entries_no_host_push)
                     int64_t open_lo = -1;
                     if (!mask.bits) {
                         open_lo = n;
@@ -1710,6 +1716,7 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
                     args.mf_hint = u.mf_hint;  // decide in the work kernel: one launch
                 } else if (push_sure) {
                     args.host_dir = 1;  // one launch, no prep
+                    g_stat_host_push.fetch_add(1, std::memory_order_relaxed);
                 } else {
                     need_prep = true;
                 }

@@ -160,6 +160,7 @@ void gb_obj_free_storage(GB_Obj *A) {
 }
 
 std::atomic<int64_t> g_stat_nvals_copy{0};
+std::atomic<int64_t> g_stat_host_push{0};
 
 int64_t gb_nvals(GB_Obj *A) {
     if (A->kind == GB_KIND_MATRIX && !A->cw) return A->nvals;
@@ -1475,7 +1476,7 @@ GrB_Info GxB_Vector_device_view(GxB_DeviceView *view, const GrB_Vector v) {
 // published to the host mailbox, so a following nvals spins instead of copying
 static void vec_recount_published(GB_Obj *o) {
     if (!o->pub) o->pub = gb_host_slot_alloc();
-    const uint64_t seq = gb_next_pub_seq();
+    const uint64_t seq = gb_next_pub_seq(o->pub);
     gb_bitmap_count_pub(o->bits, o->nrows, o->d_nvals, o->pub, seq);
     o->nvals_valid = false;
     o->hint_valid = false;

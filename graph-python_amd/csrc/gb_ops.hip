@@ -125,7 +125,7 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
     if (w->kind != GB_KIND_MATRIX) {
         if (!w->pub) w->pub = gb_host_slot_alloc();
         T.pub = w->pub;
-        T.pub_seq = gb_next_pub_seq();
+        T.pub_seq = gb_next_pub_seq(T.pub);
     }
     {
         GB_HPROF(3, "gb_spmv (host+launch)");
@@ -772,32 +772,55 @@ static void spec_drop_result() {
     g_spec.T = gb_vec_result{};
 }
 
-// undo the speculative level (g_spec_mu held); see above
+// undo the speculative level (g_spec_mu held); see above.  Never throws: the rollback runs on
+// behalf of whichever call found the speculation in its way, so a failure of the unstamp or of
+// the re-issued absorbed stamp is an execution error of v -- recorded on v (GrB_INVALID_OBJECT
+// from then on, like a failed deferred assign in gb_pending_flush), not of the calling API.
 static void spec_rollback_locked() {
     if (!g_spec.active) return;
     GB_Obj *q = g_spec.q, *v = g_spec.v;
     g_spec.active = false;
     g_spec_active.store(false, std::memory_order_release);
     g_stat_spec_rollbacks.fetch_add(1, std::memory_order_relaxed);
-    const bool q_empty = q->nvals_valid && q->nvals == 0 && q->bits == g_spec.q_bits;
-    if (!q_empty) {
-        const int64_t nw = gb_words(v->nrows);
-        hipLaunchKernelGGL(k_spec_unstamp, dim3(ops_grid(nw, 1024)), dim3(OPS_BLOCK), 0, gb_stream(), nw, v->bits,
-                           g_spec.q_bits, v->d_nvals, g_spec.q_dn, g_spec.stamp_struct ? nullptr : g_spec.q_iso,
-                           g_spec.q_iso_code);
-        GB_LAUNCH_CHECK();
+    const bool matched = g_spec.assign_matched;
+    g_spec.assign_matched = false;
+    auto record = [&](GrB_Info info, const std::string &msg) {
+        if (v->magic != GB_MAGIC) return;
+        v->invalid = info;
+        v->err = "speculative BFS level rollback failed: " + msg;
+    };
+    try {
+        const bool q_empty = q->nvals_valid && q->nvals == 0 && q->bits == g_spec.q_bits;
+        if (!q_empty) {
+            const int64_t nw = gb_words(v->nrows);
+            hipLaunchKernelGGL(k_spec_unstamp, dim3(ops_grid(nw, 1024)), dim3(OPS_BLOCK), 0, gb_stream(), nw,
+                               v->bits, g_spec.q_bits, v->d_nvals, g_spec.q_dn,
+                               g_spec.stamp_struct ? nullptr : g_spec.q_iso, g_spec.q_iso_code);
+            GB_LAUNCH_CHECK();
+        }
+        v->nvals_valid = false;
+        v->hint_valid = false;
+        if (matched) {
+            // the host issued the predicted stamp; it was absorbed: issue it now
+            // (fault injection for the tests: knob inject_spec_fail = 1)
+            GB_REQUIRE(gb_knob("inject_spec_fail") != 1, GrB_OUT_OF_MEMORY, "injected failure");
+            gb_desc ad;
+            ad.structure = g_spec.stamp_struct;
+            char xc[16] = {0};
+            memcpy(xc, &g_spec.x, sizeof(g_spec.x));
+            vector_assign_scalar(v, q, nullptr, xc, v->type->code, GrB_ALL, v->nrows, ad);
+        }
+    } catch (const gb_exception &e) {
+        record(e.info, e.msg);
+    } catch (const std::bad_alloc &) {
+        record(GrB_OUT_OF_MEMORY, "out of host memory");
+    } catch (...) {
+        record(GrB_PANIC, "unknown error");
     }
-    spec_drop_result();
-    v->nvals_valid = false;
-    v->hint_valid = false;
-    if (g_spec.assign_matched) {
-        // the host issued the predicted stamp; it was absorbed: issue it now
-        g_spec.assign_matched = false;
-        gb_desc ad;
-        ad.structure = g_spec.stamp_struct;
-        char xc[16] = {0};
-        memcpy(xc, &g_spec.x, sizeof(g_spec.x));
-        vector_assign_scalar(v, q, nullptr, xc, v->type->code, GrB_ALL, v->nrows, ad);
+    try {
+        spec_drop_result();
+    } catch (...) {
+        // freeing goes back to the caching allocator; nothing to record
     }
 }
 
@@ -828,7 +851,7 @@ static void spec_launch_locked(GB_Obj *q, GB_Obj *v, GB_Obj *A, GrB_Semiring sr,
     if (!g_spec.slot) g_spec.slot = gb_host_slot_alloc();
     gb_vec_result T;
     T.pub = g_spec.slot;
-    T.pub_seq = gb_next_pub_seq();
+    T.pub_seq = gb_next_pub_seq(T.pub);
     gb_spmv(T, V.av, V.push, V.uv, V.m, sr, vxm, &asg);
     g_spec.T = T;
     g_spec.q = q;
@@ -876,12 +899,16 @@ static void spec_after_level(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Se
 }
 
 // the host issues `w<mask> = x` (all indices, no accum): absorbed when it is the predicted stamp
+// Absorbs only what the normal path would carry out without error: GrB_ALL with ni == n, a
+// valid (not execution-failed) target and mask; anything else rolls back and takes gb_api.
 static bool spec_match_assign(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, const void *x, int xcode,
-                              const GrB_Index *I, GrB_Descriptor desc) {
+                              const GrB_Index *I, int64_t ni, GrB_Descriptor desc) {
     std::lock_guard<std::mutex> lk(g_spec_mu);
     if (!g_spec.active) return false;
     bool ok = !g_spec.assign_matched && w == g_spec.v && mask == g_spec.q && !accum && I == GrB_ALL &&
-              !g_pending_active.load(std::memory_order_acquire) && w->magic == GB_MAGIC;
+              !g_pending_active.load(std::memory_order_acquire) && w->magic == GB_MAGIC &&
+              ni == w->nrows && w->invalid == GrB_SUCCESS && mask && mask->magic == GB_MAGIC &&
+              mask->invalid == GrB_SUCCESS;
     if (ok) {
         gb_desc ad;
         try {
@@ -1473,9 +1500,17 @@ GrB_Info GrB_Semiring_new(GrB_Semiring *semiring, GrB_Monoid add, GrB_BinaryOp m
     GrB_Info GrB_Vector_assign_##T(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum, ctype x,   \
                                    const GrB_Index *I, GrB_Index ni, const GrB_Descriptor desc) {            \
         GB_HPROF(8, "GrB_Vector_assign scalar");                                                             \
-        if (g_spec_active.load(std::memory_order_acquire) && w && OBJ(w)->magic == GB_MAGIC &&             \
-            spec_match_assign(OBJ(w), mask ? OBJ(mask) : nullptr, accum, &x, GBAMD_T_##T, I, desc))         \
-            return GrB_SUCCESS; /* the predicted level stamp, already carried out (BFS speculation) */     \
+        if (g_spec_active.load(std::memory_order_acquire) && w && OBJ(w)->magic == GB_MAGIC) {             \
+            /* the predicted level stamp, already carried out (BFS speculation); the match runs   \
+               inside the API wrapper so that nothing it raises crosses the C boundary */          \
+            bool absorbed = false;                                                                           \
+            const GrB_Info mi = gb_api_impl<false>(OBJ(w), [&] {                                             \
+                absorbed = spec_match_assign(OBJ(w), mask ? OBJ(mask) : nullptr, accum, &x, GBAMD_T_##T, I, \
+                                             (int64_t)ni, desc);                                             \
+            });                                                                                              \
+            if (mi != GrB_SUCCESS) return mi;                                                                \
+            if (absorbed) return GrB_SUCCESS;                                                                \
+        }                                                                                                    \
         return gb_api(OBJ(w), [&] {                                                                          \
             vector_assign_scalar(gb_obj_check(w), gb_obj_check(mask, true), accum, &x, GBAMD_T_##T, I,       \
                                  (int64_t)ni, gb_read_desc(desc));                                           \

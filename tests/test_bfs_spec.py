@@ -306,3 +306,97 @@ def test_spec_changed_call_shape(gb, graph):
             lib.GrB_Vector_free(ctypes.byref(v))
         gb.set_knob("bfs_spec", 0)
         assert np.array_equal(results[0][0], results[1][0]) and np.array_equal(results[0][1], results[1][1])
+
+
+def test_spec_rollback_failure_is_recorded_on_v(gb, graph):
+    """the predicted stamp is absorbed, then an SpMV of another shape rolls the
+    speculation back; re-issuing the absorbed stamp fails (injected).  The failure is an
+    execution error of v -- recorded on v (GrB_INVALID_OBJECT from then on), never raised
+    across the C boundary -- and q stays usable."""
+    G, A = graph
+    n = G.nrows
+    lib = gb.lib
+    src = roots(G)[0]
+    q, v = ctypes.c_void_p(), ctypes.c_void_p()
+    ok(lib.GrB_Vector_new(ctypes.byref(q), lib.GrB_BOOL, n))
+    ok(lib.GrB_Vector_new(ctypes.byref(v), lib.GrB_INT32, n))
+    ok(lib.GrB_Vector_setElement_BOOL(q, True, src))
+    nv = U64()
+    r0 = stat(gb, "stat_bfs_spec_rollbacks")
+    try:
+        for d in range(1, 4):
+            ok(lib.GrB_Vector_assign_INT32(v, q, None, d, lib.GrB_ALL, n, None), "stamp")
+            sr = lib.GxB_ANY_PAIR_BOOL
+            if d == 3:
+                gb.set_knob("inject_spec_fail", 1)
+                sr = lib.GrB_LOR_LAND_SEMIRING_BOOL  # not the predicted SpMV: rollback
+            lib.GrB_vxm(q, v, None, sr, q, A._carg, lib.GrB_DESC_RSC)
+            gb.set_knob("inject_spec_fail", 0)
+            ok(lib.GrB_Vector_nvals(ctypes.byref(nv), q), "nvals q")
+    finally:
+        gb.set_knob("inject_spec_fail", 0)
+    assert stat(gb, "stat_bfs_spec_rollbacks") > r0
+    assert lib.GrB_Vector_nvals(ctypes.byref(nv), v) == -104  # GrB_INVALID_OBJECT
+    ok(lib.GrB_Vector_nvals(ctypes.byref(nv), q), "q stays valid")
+    lib.GrB_Vector_free(ctypes.byref(q))
+    lib.GrB_Vector_free(ctypes.byref(v))
+
+
+def test_spec_absorb_needs_valid_call(gb, graph):
+    """a stamp the normal path would treat differently (ni != n with GrB_ALL) is not
+    absorbed: the speculation rolls back and the normal path runs -- same levels as the oracle"""
+    G, A = graph
+    n = G.nrows
+    lib = gb.lib
+    src = roots(G)[0]
+    ref, _, _ = O.bfs_levels(G, src)
+    q, v = ctypes.c_void_p(), ctypes.c_void_p()
+    ok(lib.GrB_Vector_new(ctypes.byref(q), lib.GrB_BOOL, n))
+    ok(lib.GrB_Vector_new(ctypes.byref(v), lib.GrB_INT32, n))
+    ok(lib.GrB_Vector_setElement_BOOL(q, True, src))
+    nv = U64()
+    r0 = stat(gb, "stat_bfs_spec_rollbacks")
+    d = 0
+    while True:
+        d += 1
+        ok(lib.GrB_Vector_assign_INT32(v, q, None, d, lib.GrB_ALL, n + 1 if d == 3 else n, None), "stamp")
+        ok(lib.GrB_vxm(q, v, None, lib.GxB_ANY_PAIR_BOOL, q, A._carg, lib.GrB_DESC_RSC), "vxm")
+        ok(lib.GrB_Vector_nvals(ctypes.byref(nv), q))
+        if nv.value == 0:
+            break
+    got, _ = read_vec(lib, v, n)
+    assert np.array_equal(got, ref)
+    assert stat(gb, "stat_bfs_spec_rollbacks") > r0
+    lib.GrB_Vector_free(ctypes.byref(q))
+    lib.GrB_Vector_free(ctypes.byref(v))
+
+
+def test_value_mask_false_entries_no_host_push(gb, graph):
+    """the host proves push only from a lower bound on the open rows.  A value mask
+    whose stored entries are all false opens no row, so its stored count must not be read as open
+    rows (no host-decided push); the BFS's first level (v just cleared, structural stamp) is the
+    positive control: there the host does decide push."""
+    G, A = graph
+    n = G.nrows
+    lib = gb.lib
+    src = roots(G)[0]
+    h0 = stat(gb, "stat_spmv_host_push")
+    run_loop(gb, A, n, src, list(range(1, 64)))
+    assert stat(gb, "stat_spmv_host_push") > h0, "positive control: first BFS level decided on the host"
+    u, m, w = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+    ok(lib.GrB_Vector_new(ctypes.byref(u), lib.GrB_BOOL, n))
+    ok(lib.GrB_Vector_new(ctypes.byref(m), lib.GrB_BOOL, n))
+    ok(lib.GrB_Vector_new(ctypes.byref(w), lib.GrB_BOOL, n))
+    ok(lib.GrB_Vector_setElement_BOOL(u, True, src))
+    ok(lib.GrB_Vector_assign_BOOL(m, None, None, False, lib.GrB_ALL, n, None))  # n stored falses
+    nv = U64()
+    ok(lib.GrB_Vector_nvals(ctypes.byref(nv), m))
+    assert nv.value == n
+    for _ in range(2):  # the second call finds the zeroed output bitmap the first one left
+        h1 = stat(gb, "stat_spmv_host_push")
+        ok(lib.GrB_vxm(w, m, None, lib.GxB_ANY_PAIR_BOOL, u, A._carg, lib.GrB_DESC_R), "vxm")
+        ok(lib.GrB_Vector_nvals(ctypes.byref(nv), w))
+        assert nv.value == 0
+        assert stat(gb, "stat_spmv_host_push") == h1
+    for x in (u, m, w):
+        lib.GrB_Vector_free(ctypes.byref(x))
