@@ -15,6 +15,7 @@
 #include <vector>
 
 #include <cstring>
+#include <dlfcn.h>
 
 #include "gb_internal.h"
 
@@ -176,6 +177,28 @@ unsigned long long *gb_device_state() {
 
 // ---- host-time probes (gb_internal.h)
 bool g_hprof_on = getenv("GRAPHBLAS_AMD_HPROF") != nullptr;
+
+// ---- roctx ranges (gb_internal.h: gb_roctx_range)
+namespace {
+int (*p_roctx_push)(const char *) = nullptr;
+int (*p_roctx_pop)() = nullptr;
+bool roctx_init() {
+    const char *e = getenv("GRAPHBLAS_AMD_ROCTX");
+    if (!e || strcmp(e, "1") != 0) return false;
+    void *h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("librocprofiler-sdk-roctx.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+        fprintf(stderr, "graphblas_amd: GRAPHBLAS_AMD_ROCTX=1 but the roctx library is not loadable\n");
+        return false;
+    }
+    p_roctx_push = (int (*)(const char *))dlsym(h, "roctxRangePushA");
+    p_roctx_pop = (int (*)())dlsym(h, "roctxRangePop");
+    return p_roctx_push && p_roctx_pop;
+}
+}  // namespace
+bool g_roctx_on = roctx_init();
+void gb_roctx_push(const char *name) { p_roctx_push(name); }
+void gb_roctx_pop() { p_roctx_pop(); }
 namespace {
 struct hprof_slot {
     std::atomic<int64_t> ns{0}, calls{0};

@@ -135,49 +135,115 @@ __device__ __forceinline__ int64_t dt_lower(const int32_t *__restrict__ v, int64
     return lo;
 }
 
-__global__ void k_dt_piece_flags(dt_side s, int64_t nh, int piece, int cap, const int32_t *__restrict__ hG,
-                                 const int64_t *__restrict__ hYS, const int32_t *__restrict__ hB,
-                                 uint8_t *__restrict__ cnt, int64_t *__restrict__ pys, int32_t *__restrict__ pb) {
+// The hub entries come in G order (hG ascending); the hub entries of group g are [h0, h1).
+// Pairs (entry, piece) are numbered group by group, piece-major inside a group -- pair
+// (i, j) = P[h0] + j * (h1 - h0) + (i - h0), P the exclusive scan of the entries' piece
+// counts -- so a group's entries of one piece are consecutive (its tasks share that piece's
+// keys in LDS) and the pair space is exactly the pieces the entries have (the
+// round-4 piece-major layout was nh x the longest list's piece count).
+__device__ __forceinline__ void dt_group_span(const int32_t *__restrict__ hG, int64_t nh, int64_t i, int64_t &h0,
+                                              int64_t &h1) {
+    const int32_t g = hG[i];
+    int64_t lo = 0, hi = i;  // first index with hG == g
+    while (lo < hi) {
+        const int64_t m = (lo + hi) >> 1;
+        if (hG[m] < g) lo = m + 1;
+        else hi = m;
+    }
+    h0 = lo;
+    lo = i + 1;
+    hi = nh;  // first index with hG > g
+    while (lo < hi) {
+        const int64_t m = (lo + hi) >> 1;
+        if (hG[m] <= g) lo = m + 1;
+        else hi = m;
+    }
+    h1 = lo;
+}
+
+__global__ void k_dt_piece_count(dt_side s, int64_t nh, int cap, const int32_t *__restrict__ hG,
+                                 int64_t *__restrict__ npc) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nh; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t g = hG[i], xs = s.xrp[g], a = s.xrp[g + 1] - xs, x0 = (int64_t)piece * cap;
-        uint8_t c = 0;
-        if (x0 < a) {
-            const int64_t x1 = (x0 + cap < a ? x0 + cap : a) - 1;
-            const int32_t k0 = s.xci[xs + x0], k1 = s.xci[xs + x1];
-            const int64_t ys = hYS[i], ye = ys + hB[i];
-            const int64_t lo = dt_lower(s.yci, ys, ye, k0);
-            const int64_t hi = k1 == INT32_MAX ? ye : dt_lower(s.yci, lo, ye, k1 + 1);
-            pys[i] = lo;
-            pb[i] = (int32_t)(hi - lo);
-            c = (uint8_t)((hi - lo + cap - 1) / cap);
-        }
-        cnt[i] = c;
+        const int64_t g = hG[i], a = s.xrp[g + 1] - s.xrp[g];
+        npc[i] = (a + cap - 1) / cap;
     }
 }
 
-// all pieces at once: pair q = j * nh + i (piece-major, so a group's entries of one piece are
-// consecutive and its tasks share that piece's keys); ePc[e] = the piece
-__global__ void k_dt_piece_compact(int64_t nh, int64_t npairs, int cap, const uint8_t *__restrict__ cnt,
-                                   const int64_t *__restrict__ pos, const int32_t *__restrict__ hG,
-                                   const int32_t *__restrict__ hO, const int64_t *__restrict__ hQ,
+// per pair: the entry's run of Y keys inside the piece's key range (two binary searches; the
+// runs of consecutive pieces follow each other, so each search starts where the last ended),
+// cut into sub-entries of at most cap keys (the task kernel's flat-space bound)
+__global__ void k_dt_piece_flags(dt_side s, int64_t nh, int cap, const int32_t *__restrict__ hG,
+                                 const int64_t *__restrict__ hYS, const int32_t *__restrict__ hB,
+                                 const int64_t *__restrict__ P, int32_t *__restrict__ cnt, int64_t *__restrict__ pys,
+                                 int32_t *__restrict__ pb) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nh; i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t h0, h1;
+        dt_group_span(hG, nh, i, h0, h1);
+        const int64_t g = hG[i], xs = s.xrp[g], a = s.xrp[g + 1] - xs;
+        const int64_t base = P[h0] + (i - h0), m = h1 - h0, np = P[i + 1] - P[i];
+        const int64_t ye = hYS[i] + hB[i];
+        int64_t lo = hYS[i];
+        for (int64_t j = 0; j < np; j++) {
+            const int64_t x0 = j * cap, x1 = (x0 + cap < a ? x0 + cap : a) - 1;
+            const int32_t k0 = s.xci[xs + x0], k1 = s.xci[xs + x1];
+            lo = dt_lower(s.yci, lo, ye, k0);
+            const int64_t hi = k1 == INT32_MAX ? ye : dt_lower(s.yci, lo, ye, k1 + 1);
+            const int64_t q = base + j * m;
+            pys[q] = lo;
+            pb[q] = (int32_t)(hi - lo);
+            cnt[q] = (int32_t)((hi - lo + cap - 1) / cap);
+            lo = hi;
+        }
+    }
+}
+
+// every pair's sub-entries at its scanned position; ePc[e] = the piece
+__global__ void k_dt_piece_compact(int64_t nh, int cap, const int32_t *__restrict__ hG, const int32_t *__restrict__ hO,
+                                   const int64_t *__restrict__ hQ, const int64_t *__restrict__ P,
+                                   const int32_t *__restrict__ cnt, const int64_t *__restrict__ ppos,
                                    const int64_t *__restrict__ pys, const int32_t *__restrict__ pb,
                                    int32_t *__restrict__ eG, int64_t *__restrict__ eYS, int32_t *__restrict__ eO,
                                    int32_t *__restrict__ eB, int64_t *__restrict__ eQ, uint16_t *__restrict__ ePc) {
-    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < npairs;
-         q += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = q % nh;
-        const uint16_t j = (uint16_t)(q / nh);
-        for (int c = 0; c < cnt[q]; c++) {
-            const int64_t e = pos[q] + c;
-            const int64_t o0 = (int64_t)c * cap;
-            eG[e] = hG[i];
-            eYS[e] = pys[q] + o0;
-            eO[e] = hO[i];
-            eB[e] = (int32_t)(pb[q] - o0 < cap ? pb[q] - o0 : cap);
-            eQ[e] = hQ[i];
-            ePc[e] = j;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nh; i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t h0, h1;
+        dt_group_span(hG, nh, i, h0, h1);
+        const int64_t base = P[h0] + (i - h0), m = h1 - h0, np = P[i + 1] - P[i];
+        const int32_t g = hG[i], o = hO[i];
+        const int64_t qq = hQ[i];
+        for (int64_t j = 0; j < np; j++) {
+            const int64_t q = base + j * m;
+            for (int c = 0; c < cnt[q]; c++) {
+                const int64_t e = ppos[q] + c;
+                const int64_t o0 = (int64_t)c * cap;
+                eG[e] = g;
+                eYS[e] = pys[q] + o0;
+                eO[e] = o;
+                eB[e] = (int32_t)(pb[q] - o0 < cap ? pb[q] - o0 : cap);
+                eQ[e] = qq;
+                ePc[e] = (uint16_t)j;
+            }
         }
     }
+}
+
+// Y-blocked task order (knob dot_yblk = K > 1): the task entries are stably partitioned by
+// which K-th of the Y matrix's entries their Y list starts in, so that at any time the
+// workgroups stream Y lists (keys and values) from one K-th of Y -- a working set the
+// Infinity Cache / L2 can hold -- instead of from all of it.  X lists are reloaded once
+// per block they have entries in.
+__global__ void k_dt_ykey(int64_t ne, int K, int64_t ytot, const int64_t *__restrict__ eYS, int32_t *__restrict__ key,
+                          int64_t *__restrict__ idx) {
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = ytot > 0 ? (int64_t)(((__int128)eYS[e] * K) / ytot) : 0;
+        key[e] = (int32_t)(b < K ? b : K - 1);
+        idx[e] = e;
+    }
+}
+
+template <class T>
+__global__ void k_dt_gather(int64_t ne, const int64_t *__restrict__ idx, const T *__restrict__ src, T *__restrict__ dst) {
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x)
+        dst[e] = src[idx[e]];
 }
 
 // huge entries left to the per-entry kernel: G-order flags -> CSR-order flags
@@ -747,6 +813,33 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
             auto run_tasks = [&](int64_t ne, int32_t *eG, int64_t *eYS, int32_t *eO, int32_t *eB, int64_t *eQ,
                                  const uint16_t *ePc) {
                 gb_scratch ts;
+                const int64_t K = gb_knob("dot_yblk");
+                if (K > 1 && K <= 4096 && ne > 1) {
+                    int bits = 0;
+                    while ((1LL << bits) < K) bits++;
+                    int32_t *key = ts.get<int32_t>(ne);
+                    int64_t *idx = ts.get<int64_t>(ne);
+                    const int64_t ytot = gb_read_i64(sd.yrp + (SWAP ? A.nrows : BT.nrows));
+                    hipLaunchKernelGGL(k_dt_ykey, dim3(dt_grid(ne)), dim3(DT_BLOCK), 0, gb_stream(), ne, (int)K, ytot,
+                                       eYS, key, idx);
+                    GB_LAUNCH_CHECK();
+                    gb_sort_pairs_i32(key, idx, ne, bits);  // stable: G order inside a block
+                    auto perm = [&](auto *arr) {
+                        using T = std::remove_pointer_t<decltype(arr)>;
+                        T *tmp = gb_malloc_n<T>(ne);
+                        hipLaunchKernelGGL(k_dt_gather<T>, dim3(dt_grid(ne)), dim3(DT_BLOCK), 0, gb_stream(), ne, idx,
+                                           (const T *)arr, tmp);
+                        GB_LAUNCH_CHECK();
+                        gb_copy_d2d(arr, tmp, ne * sizeof(T));
+                        gb_free(tmp);
+                    };
+                    perm(eG);
+                    perm(eYS);
+                    perm(eO);
+                    perm(eB);
+                    perm(eQ);
+                    if (ePc) perm(const_cast<uint16_t *>(ePc));
+                }
                 int64_t *cum = ts.get<int64_t>(ne + 1);
                 gb_exclusive_scan_i32(eB, (int)ovh, cum, ne);
                 uint8_t *tsf = ts.get<uint8_t>(ne);
@@ -828,18 +921,26 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
                 GB_LAUNCH_CHECK();
                 return;
             }
-            // every piece's runs at once (pairs piece-major): one scan, one compaction, one task
-            // launch (round 4: one pass per piece, each ending on a host read of its size)
-            const int64_t npairs = nh * np;
-            uint8_t *pc = hs.get<uint8_t>(npairs);
+            // every piece's runs at once: one scan, one compaction, one task launch (round 4: one
+            // pass per piece, each ending on a host read of its size); scratch in proportion to the
+            // pieces the entries have (pairs numbered group by group, see dt_group_span)
+            int64_t *P = hs.get<int64_t>(nh + 1);
+            {
+                int64_t *npc = hs.get<int64_t>(nh);
+                hipLaunchKernelGGL(k_dt_piece_count, dim3(dt_grid(nh)), dim3(DT_BLOCK), 0, gb_stream(), sd, nh, cap,
+                                   hG, npc);
+                GB_LAUNCH_CHECK();
+                gb_exclusive_scan_i64(npc, P, nh);
+            }
+            const int64_t npairs = gb_read_i64(P + nh);
+            int32_t *pc = hs.get<int32_t>(npairs);
             int64_t *ppos = hs.get<int64_t>(npairs + 1);
             int64_t *pys = hs.get<int64_t>(npairs);
             int32_t *pb = hs.get<int32_t>(npairs);
-            for (int j = 0; j < np; j++)
-                hipLaunchKernelGGL(k_dt_piece_flags, dim3(dt_grid(nh)), dim3(DT_BLOCK), 0, gb_stream(), sd, nh, j,
-                                   cap, hG, hYS, hB, pc + j * nh, pys + j * nh, pb + j * nh);
+            hipLaunchKernelGGL(k_dt_piece_flags, dim3(dt_grid(nh)), dim3(DT_BLOCK), 0, gb_stream(), sd, nh, cap, hG,
+                               hYS, hB, P, pc, pys, pb);
             GB_LAUNCH_CHECK();
-            gb_exclusive_scan_u8(pc, ppos, npairs);
+            gb_exclusive_scan_i32(pc, 0, ppos, npairs);
             const int64_t npe = gb_read_i64(ppos + npairs);
             if (npe == 0) return;
             gb_scratch ps;
@@ -849,8 +950,8 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
             int32_t *eB = ps.get<int32_t>(npe);
             int64_t *eQ = ps.get<int64_t>(npe);
             uint16_t *ePc = ps.get<uint16_t>(npe);
-            hipLaunchKernelGGL(k_dt_piece_compact, dim3(dt_grid(npairs)), dim3(DT_BLOCK), 0, gb_stream(), nh, npairs,
-                               cap, pc, ppos, hG, hO, hQ, pys, pb, eG, eYS, eO, eB, eQ, ePc);
+            hipLaunchKernelGGL(k_dt_piece_compact, dim3(dt_grid(nh)), dim3(DT_BLOCK), 0, gb_stream(), nh, cap, hG, hO,
+                               hQ, P, pc, ppos, pys, pb, eG, eYS, eO, eB, eQ, ePc);
             GB_LAUNCH_CHECK();
             run_tasks(npe, eG, eYS, eO, eB, eQ, ePc);
         };

@@ -179,8 +179,26 @@ struct gb_spec_hold_guard {
     ~gb_spec_hold_guard() { g_spec_hold--; }
 };
 
+// roctx ranges named by the API entry point around each library call (environment
+// GRAPHBLAS_AMD_ROCTX=1; the roctx library is loaded then, never otherwise), so a rocprofv3
+// trace with --marker-trace attributes every kernel to the GrB_* / GxB_* call that launched
+// it -- the kernel-level counterpart of the reference's Recorder (core/recorder.py:34-178).
+extern bool g_roctx_on;
+void gb_roctx_push(const char *name);
+void gb_roctx_pop();
+struct gb_roctx_range {
+    bool on;
+    explicit gb_roctx_range(const char *name) : on(g_roctx_on && name) {
+        if (on) gb_roctx_push(name);
+    }
+    ~gb_roctx_range() {
+        if (on) gb_roctx_pop();
+    }
+};
+
 template <bool FLUSH = true, class F>
-GrB_Info gb_api_impl(GB_Obj *errobj, F &&body) {
+GrB_Info gb_api_impl(GB_Obj *errobj, F &&body, const char *name = nullptr) {
+    gb_roctx_range range(name);
     try {
         if (FLUSH && !g_spec_hold && g_spec_active.load(std::memory_order_acquire)) gb_spec_resolve(nullptr);
         if (FLUSH && g_pending_active.load(std::memory_order_acquire)) gb_pending_flush();
@@ -198,14 +216,17 @@ GrB_Info gb_api_impl(GB_Obj *errobj, F &&body) {
     }
 }
 template <class F>
-GrB_Info gb_api(GB_Obj *errobj, F &&body) {
-    return gb_api_impl<true>(errobj, std::forward<F>(body));
+GrB_Info gb_api_named(const char *name, GB_Obj *errobj, F &&body) {
+    return gb_api_impl<true>(errobj, std::forward<F>(body), name);
 }
 // GrB_mxv / GrB_vxm: the deferred assign is fused or flushed inside (do_spmv)
 template <class F>
-GrB_Info gb_api_keep_pending(GB_Obj *errobj, F &&body) {
-    return gb_api_impl<false>(errobj, std::forward<F>(body));
+GrB_Info gb_api_keep_pending_named(const char *name, GB_Obj *errobj, F &&body) {
+    return gb_api_impl<false>(errobj, std::forward<F>(body), name);
 }
+// the entry point's own name (__func__) names its trace range
+#define gb_api(obj, ...) gb_api_named(__func__, obj, __VA_ARGS__)
+#define gb_api_keep_pending(obj, ...) gb_api_keep_pending_named(__func__, obj, __VA_ARGS__)
 
 // ------------------------------------------------------------------ host-time probes
 // Diagnostics of the per-call host path (environment GRAPHBLAS_AMD_HPROF=1): cumulative

@@ -825,9 +825,11 @@ TWO_SIDED = [
 
 
 @pytest.mark.parametrize("name,mon,mul,dt", TWO_SIDED)
-# (dot_cap, dot_win, dot_pieces): defaults; short task windows; a cap of 300 keys, so the
-# hub lists run as pieces (default) or on the per-entry kernel (dot_pieces = 1)
-@pytest.mark.parametrize("knobs", [(0, 0, 0), (128, 256, 0), (300, 256, 0), (300, 256, 1)])
+# (dot_cap, dot_win, dot_pieces, dot_yblk): defaults; short task windows; a cap of 300 keys, so
+# the hub lists run as pieces (default) or on the per-entry kernel (dot_pieces = 1); tasks in
+# Y-blocked order (8 / 3 blocks)
+@pytest.mark.parametrize("knobs", [(0, 0, 0, 0), (128, 256, 0, 0), (300, 256, 0, 0), (300, 256, 1, 0),
+                                   (300, 256, 0, 8), (0, 0, 0, 3)])
 @pytest.mark.parametrize("form", ["AA_struct", "AAT_struct", "ATA_value", "AB_rect"])
 def test_masked_spgemm_two_sided_vs_oracle(gb, name, mon, mul, dt, knobs, form):
     """The two-sided LDS masked dot (gb_dot.hip): entries grouped by the side owning the
@@ -840,7 +842,8 @@ def test_masked_spgemm_two_sided_vs_oracle(gb, name, mon, mul, dt, knobs, form):
     Ao = _skewed_both(rng, n, dt)
     sr = getattr(gb.semiring, name)[dt]
     Ag = _to_gb(gb, Ao)
-    cap, win, pieces = knobs
+    cap, win, pieces, yblk = knobs
+    gb.set_knob("dot_yblk", yblk)
     gb.set_knob("dot_cap", cap)
     gb.set_knob("dot_win", win)
     gb.set_knob("dot_pieces", pieces)
@@ -876,6 +879,7 @@ def test_masked_spgemm_two_sided_vs_oracle(gb, name, mon, mul, dt, knobs, form):
         gb.set_knob("dot_win", 0)
         gb.set_knob("dot_pieces", 0)
         gb.set_knob("dot_pmin", 0)
+        gb.set_knob("dot_yblk", 0)
     if mon == "ANY":
         r, c, _ = Cg.to_coo()
         er, ec, _ = ref.to_coo()
