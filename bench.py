@@ -63,6 +63,8 @@ def parse():
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r04.json"))
     # rehearsal of the N>1 path on one GPU: all ranks on one device, gloo transport
     p.add_argument("--dist-backend", default="nccl")
+    p.add_argument("--no-pipeline", action="store_true",
+                   help="N > 1: wait for each level's count before enqueuing the next (round-4 loop)")
     p.add_argument("--partition", default="balanced", choices=["balanced", "equal"],
                    help="N > 1 BFS: vertex ranges balanced by the shards' entries, or equal word slots")
     p.add_argument("--device", type=int, default=None, help="override LOCAL_RANK's device")
@@ -889,8 +891,10 @@ def main():
     qloc = ctypes.c_void_p()
     ok(lib.GrB_Vector_new(ctypes.byref(q), lib.GrB_BOOL, n), "q")
     ok(lib.GrB_Vector_new(ctypes.byref(v), lib.GrB_INT32, nloc), "v")
+    q2 = ctypes.c_void_p()  # the second frontier buffer of the pipelined sharded loop
     if world > 1:
         ok(lib.GrB_Vector_new(ctypes.byref(qloc), lib.GrB_BOOL, nloc), "qloc")
+        ok(lib.GrB_Vector_new(ctypes.byref(q2), lib.GrB_BOOL, n), "q2")
         exchange = gdist.BitmapAllGather(dist, part, world, "cuda")
     nv = ctypes.c_uint64()
     ev_pairs, level_counts = [], []
@@ -899,15 +903,51 @@ def main():
     # slots that tile the words exactly, or packed ranges (balanced bounds)
     zero_copy = world > 1 and (part.get("bounds") is not None or part["slot"] * world == words)
 
-    def exchange_frontier(into_q_bits):
-        """all-gather the ranks' frontier slices (RCCL, on the library stream) into q"""
+    def exchange_frontier(into_q_bits, qv=None):
+        """all-gather the ranks' frontier slices (RCCL, on the library stream) into qv (q)"""
+        qv = q if qv is None else qv
         ok(lib.GxB_Vector_bitmap_export(qloc, ctypes.c_void_p(exchange.send.data_ptr()), hi_w - lo_w), "bm out")
         with torch.cuda.stream(stream):
             gath = exchange.run(into_q_bits)  # into_q_bits: straight into q's device bitmap
         if into_q_bits is not None:
-            ok(lib.GxB_Vector_device_touch(q), "touch q")
+            ok(lib.GxB_Vector_device_touch(qv), "touch q")
         else:
-            ok(lib.GxB_Vector_bitmap_import(q, ctypes.c_void_p(gath.data_ptr()), words), "bm in")
+            ok(lib.GxB_Vector_bitmap_import(qv, ctypes.c_void_p(gath.data_ptr()), words), "bm in")
+
+    def sharded_levels_pipelined(timing):
+        """N > 1, default: the level loop with the host one level behind the device
+        (gdist.pipelined_levels) -- level d + 1's stamp, shard SpMV, all-gather
+        and recount are enqueued before the host waits for level d's count (publish ticket)"""
+        bufs = [q, q2]
+        views = [None, None]
+        if zero_copy:
+            from graphblas_amd import device as gdev
+
+            views = [gdev.device_tensor(torch, gdev.vector_view(b).bitmap, words) for b in bufs]
+        first = {1: True}  # q2's first exchange of a BFS goes through bitmap_import (iso true)
+
+        def enqueue(d):
+            ok(lib.GrB_Vector_assign_INT32(v, qloc, None, d, grb_all, nloc, None), "assign")
+            if timing:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            ok(lib.GrB_mxv(qloc, v, None, sr_box[0], A, bufs[(d - 1) % 2], desc), "mxv")
+            if timing:
+                e1.record(stream)
+                ev_pairs.append((e0, e1))
+            tgt = d % 2
+            exchange_frontier(None if first.pop(tgt, False) else views[tgt], bufs[tgt])
+            t = ctypes.c_uint64()
+            ok(lib.GxB_Vector_publish_ticket(ctypes.byref(t), bufs[tgt]), "ticket")
+            return bufs[tgt], t.value
+
+        def count_of(tok):
+            c = ctypes.c_uint64()
+            ok(lib.GxB_Vector_wait_ticket(ctypes.byref(c), tok[0], ctypes.c_uint64(tok[1])), "wait ticket")
+            return c.value
+
+        return gdist.pipelined_levels(enqueue, count_of, max_levels=n + 2)
 
     def bfs(src, timing):
         ok(lib.GrB_Vector_clear(q), "clear q")
@@ -920,6 +960,10 @@ def main():
             if lo <= src < hi:
                 ok(lib.GrB_Vector_setElement_BOOL(qloc, True, int(src) - lo), "qloc[src]")
             exchange_frontier(None)  # q = root, iso true
+            if not args.no_pipeline:
+                d = sharded_levels_pipelined(timing)
+                level_counts.append(d)
+                return d
             if zero_copy:
                 from graphblas_amd import device as gdev
 

@@ -1491,6 +1491,29 @@ GrB_Info GxB_Vector_device_touch(GrB_Vector v) {
         vec_recount_published(o);
     });
 }
+// The ticket of v's last device publish and a wait on it (include/graphblas_amd.h): the count
+// v had at that publish, read from the host mailbox even after later work that does not write
+// v has been enqueued (nvals itself trusts a mailbox only while nothing was enqueued since).
+GrB_Info GxB_Vector_publish_ticket(uint64_t *ticket, GrB_Vector v) {
+    if (!ticket) return GrB_NULL_POINTER;
+    return gb_api(OBJ(v), [&] {
+        GB_Obj *o = gb_obj_check(v);
+        GB_REQUIRE(o->kind != GB_KIND_MATRIX, GrB_INVALID_OBJECT, "not a vector");
+        *ticket = o->pub ? o->pub_seq : 0;
+    });
+}
+GrB_Info GxB_Vector_wait_ticket(GrB_Index *nvals, GrB_Vector v, uint64_t ticket) {
+    if (!nvals) return GrB_NULL_POINTER;
+    return gb_api(OBJ(v), [&] {
+        GB_Obj *o = gb_obj_check(v);
+        GB_REQUIRE(o->kind != GB_KIND_MATRIX, GrB_INVALID_OBJECT, "not a vector");
+        GB_REQUIRE(o->pub && ticket, GrB_INVALID_VALUE, "no device publish to wait for");
+        int64_t c = 0;
+        GB_REQUIRE(gb_host_slot_wait(o->pub, ticket, &c), GrB_INVALID_VALUE,
+                   "the publish was superseded by a later one of the same vector");
+        *nvals = (GrB_Index)c;
+    });
+}
 GrB_Info GxB_Vector_bitmap_export(GrB_Vector v, void *dst, GrB_Index nwords) {
     return gb_api(OBJ(v), [&] {
         GB_Obj *o = gb_obj_check(v);

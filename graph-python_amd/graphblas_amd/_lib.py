@@ -73,6 +73,7 @@ _SIGS = {
     "GrB_Vector_extract": [P, P, P, P, P, I, P], "GxB_Global_Option_get_INT32": [E, P],
     "GxB_Matrix_device_view": [P, P], "GxB_Vector_device_view": [P, P],
     "GxB_Vector_device_touch": [P], "GxB_Matrix_prepare_transpose": [P],
+    "GxB_Vector_publish_ticket": [P, P], "GxB_Vector_wait_ticket": [P, P, U],
     "GxB_Matrix_rmat": [P, E, E, U, E, U, I, I],
     "GxB_Vector_bitmap_export": [P, P, I], "GxB_Vector_bitmap_import": [P, P, I],
     "GxB_Matrix_import_device": [P, P, I, I, P, P, P, I, ctypes.c_bool],

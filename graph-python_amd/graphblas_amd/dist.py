@@ -101,6 +101,35 @@ def word_sums(torch, row_w, nwords):
     return pad.view(nwords, 64).sum(1)
 
 
+def pipelined_levels(enqueue, count_of, max_levels=None):
+    """The level loop of reference notebooks/Example B.1 cell 8 (`v<q.V> = d; q<!v.S, replace> =
+    q (+).(x) A; if q.nvals == 0: break`) with the host one level behind the device (DESIGN.md
+    §6): level d + 1 is enqueued before the host waits for level d's frontier count, so the
+    next level's launches, all-gather and recount are already queued on the stream while the
+    host reads the count -- the sharded loop's counterpart of the library's single-GPU level
+    speculation, which needs w == u and so never runs on a shard.
+
+    enqueue(d) enqueues level d: the stamp d over the current frontier, the local SpMV and the
+    exchange into the other of two frontier buffers (level d reads buffer (d - 1) % 2 and
+    writes buffer d % 2, so the buffer whose count the host is waiting for is written again only
+    by a level enqueued after that wait); it returns a token for the frontier it produces.
+    count_of(token) waits for that frontier's size (GxB_Vector_wait_ticket on a GPU).  A level
+    over an empty frontier stamps nothing and produces an empty frontier, so the one level
+    enqueued past the end changes nothing.  Returns the number of levels, as the plain loop's
+    d at its break."""
+    d = 1
+    tok = enqueue(1)
+    while True:
+        if max_levels is not None and d >= max_levels:
+            count_of(tok)
+            return d
+        nxt = enqueue(d + 1)
+        if count_of(tok) == 0:
+            return d
+        d += 1
+        tok = nxt
+
+
 class BitmapAllGather:
     """All-gather of int64 bitmap slices into one frontier bitmap.
 

@@ -403,6 +403,17 @@ GrB_Info GxB_Matrix_import_device(GrB_Matrix *A, GrB_Type type, GrB_Index nrows,
 /* Mark that the vector's bitmap/values were rewritten through a device view
  * (nvals recomputed on device, on the library stream). */
 GrB_Info GxB_Vector_device_touch(GrB_Vector v);
+/* The ticket of the vector's last device publish of its count (0: none; device_touch,
+ * bitmap_import and the SpMV kernels publish), and a wait on it: *nvals = the count the
+ * vector had at that publish, read from the pinned host mailbox without synchronising the
+ * stream -- valid although later work that does not write the vector was enqueued since
+ * (GrB_Vector_nvals trusts a mailbox only while nothing was).  GrB_INVALID_VALUE if a later
+ * publish of the same vector superseded it.  The pipelined sharded level loop
+ * (graphblas_amd/dist.py: PipelinedLevels) enqueues level d + 1 before it waits for level
+ * d's frontier count.  Replaces the nvals read of reference notebooks/Example B.1 cell 8
+ * (`q.nvals`, core/vector.py: Vector.nvals -> GrB_Vector_nvals). */
+GrB_Info GxB_Vector_publish_ticket(uint64_t *ticket, GrB_Vector v);
+GrB_Info GxB_Vector_wait_ticket(GrB_Index *nvals, GrB_Vector v, uint64_t ticket);
 /* Copy the first nwords 64-bit words of a vector's presence bitmap to /
  * from device memory on the library stream (frontier exchange over RCCL).
  * Import makes the vector iso-valued 1 (true) on every set bit. */

@@ -159,3 +159,102 @@ def test_balanced_bounds_even_out_a_skewed_graph():
             covered[p["lo"]:p["hi"]] += 1
             assert p["hi_w"] - p["lo_w"] <= p["slot"]
         assert (covered == 1).all()
+
+
+def _worker_pipelined(rank, world, port, scale, src, out_q, balanced):
+    """The sharded loop with the host one level behind (gdist.pipelined_levels): level d + 1 is
+    enqueued -- stamp, local pull step, all-gather into the other frontier buffer -- before the
+    count of level d's frontier is read.  Same numpy local step as _worker."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    G = _graph(scale, balanced)
+    n = G.nrows
+    AT = _transpose(G)
+    bounds = None
+    if balanced:
+        words = (n + 63) // 64
+        deg = np.zeros(words * 64, np.int64)
+        deg[:n] = np.diff(AT.indptr)
+        bounds = gdist.balanced_bounds(deg.reshape(words, 64).sum(1), world)
+    part = gdist.partition(n, world, rank, bounds)
+    lo, hi = part["lo"], part["hi"]
+    ex = gdist.BitmapAllGather(dist, part, world, "cpu")
+    bufs = [np.zeros(n, bool), np.zeros(n, bool)]  # the two frontier buffers (q_a, q_b)
+    bufs[0][src] = True
+    qloc = bufs[0][lo:hi].copy()  # this rank's slice of the current frontier (the stamp's mask)
+    visited = np.zeros(hi - lo, bool)
+    level = np.zeros(hi - lo, np.int32)
+    issued = []
+
+    def enqueue(d):
+        nonlocal qloc
+        issued.append(d)
+        cur, nxt_buf = bufs[(d - 1) % 2], bufs[d % 2]
+        level[qloc & ~visited] = d  # v<qloc> = d
+        visited[:] |= qloc
+        nxt = np.zeros(hi - lo, bool)  # qloc<!v.S, replace> = A^T_r lor.land q
+        for r in range(lo, hi):
+            if not visited[r - lo]:
+                cols = AT.indices[AT.indptr[r]:AT.indptr[r + 1]]
+                nxt[r - lo] = bool(cur[cols].any())
+        qloc = nxt
+        ex.send.copy_(torch.from_numpy(gdist.pack_bits(nxt, part["slot"])))
+        full = ex.run().numpy()
+        if bounds is not None:
+            nxt_buf[:] = gdist.unpack_bits(full[:part["words"]], n)
+        else:
+            nxt_buf[:] = False
+            for k in range(world):
+                pk = gdist.partition(n, world, k)
+                sl = full[k * part["slot"]:k * part["slot"] + (pk["hi_w"] - pk["lo_w"])]
+                nxt_buf[pk["lo"]:pk["hi"]] = gdist.unpack_bits(sl, pk["hi"] - pk["lo"])
+        return int(nxt_buf.sum())  # the token: the device-published count
+
+    nlev = gdist.pipelined_levels(enqueue, lambda tok: tok, max_levels=n + 2)
+    out_q.put((rank, lo, hi, level, nlev, issued))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("scale,world,balanced", [(9, 2, False), (10, 2, True), (9, 3, True)])
+def test_pipelined_sharded_bfs_matches_oracle(scale, world, balanced):
+    """the sharded level loop with the host one level behind the device gives the
+    oracle's levels; it issues exactly one level past the last (over an empty frontier, a no-op)."""
+    G = _graph(scale, balanced)
+    src = int(np.argmax(np.diff(G.indptr)))
+    ref, nref, _ = O.bfs_levels(G, src)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_pipelined, args=(r, world, port, scale, src, q, balanced))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = np.zeros(G.nrows, np.int32)
+    for _ in range(world):
+        rank, lo, hi, level, nlev, issued = q.get(timeout=120)
+        got[lo:hi] = level
+        assert issued == list(range(1, nlev + 2))
+        assert nlev == int(ref.max())
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert np.array_equal(got, ref)
+
+
+def test_pipelined_levels_order():
+    """the driver alone: level d + 1 is enqueued before level d's count is read"""
+    log = []
+    counts = {1: 3, 2: 5, 3: 0}
+
+    def enqueue(d):
+        log.append(("enqueue", d))
+        return d
+
+    def count_of(d):
+        log.append(("count", d))
+        return counts.get(d, 0)
+
+    assert gdist.pipelined_levels(enqueue, count_of) == 3
+    assert log == [("enqueue", 1), ("enqueue", 2), ("count", 1), ("enqueue", 3), ("count", 2),
+                   ("enqueue", 4), ("count", 3)]

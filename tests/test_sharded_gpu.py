@@ -132,6 +132,111 @@ def test_sharded_bfs_mxv_vs_oracle(env, scale, world, exchange, semiring):
         ok(lib.GrB_Vector_free(ctypes.byref(h)), "free")
 
 
+@pytest.mark.parametrize("scale", [10, 14])
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_bfs_pipelined_vs_oracle(env, scale, world):
+    """bench.py's N > 1 loop as it runs by default: two frontier buffers, the
+    host one level behind the device (graphblas_amd.dist.pipelined_levels) -- level d + 1's
+    stamps, shard SpMVs, exchange and recount are enqueued before the host waits for level d's
+    count through its publish ticket (GxB_Vector_publish_ticket / GxB_Vector_wait_ticket), which
+    stays readable although level d + 1 was enqueued behind it.  Levels bit-exact vs the
+    oracle; exactly one level is issued past the last."""
+    gb, torch, stream = env
+    from graphblas_amd import device as gdev
+    from graphblas_amd import dist as gdist
+
+    lib = gb.lib
+    n = 1 << scale
+    G = O.rmat(scale, 16, 42)
+    deg = np.diff(G.indptr)
+    parts = [gdist.partition(n, world, r) for r in range(world)]
+    words, slot = parts[0]["words"], parts[0]["slot"]
+    AT, v, ql = [], [], []
+    for p in parts:
+        nloc = p["hi"] - p["lo"]
+        h = ctypes.c_void_p()
+        ok(lib.GxB_Matrix_rmat(ctypes.byref(h), scale, 16, 42, 0x100, 0, p["lo"], p["hi"]), "rmat shard")
+        AT.append(h)
+        for lst, t in ((v, lib.GrB_INT32), (ql, lib.GrB_BOOL)):
+            x = ctypes.c_void_p()
+            ok(lib.GrB_Vector_new(ctypes.byref(x), t, nloc), "new")
+            lst.append(x)
+    bufs = []
+    for _ in range(2):
+        x = ctypes.c_void_p()
+        ok(lib.GrB_Vector_new(ctypes.byref(x), lib.GrB_BOOL, n), "q")
+        bufs.append(x)
+    staged = torch.zeros(slot * world, dtype=torch.int64, device="cuda")
+    sr = lib.GxB_ANY_PAIR_BOOL
+    nv = ctypes.c_uint64()
+
+    def gather_into(q, via_import):
+        if via_import:  # the buffer's first exchange of a BFS makes it iso true
+            for r, p in enumerate(parts):
+                cnt = p["hi_w"] - p["lo_w"]
+                if cnt:
+                    ok(lib.GxB_Vector_bitmap_export(ql[r], ctypes.c_void_p(staged.data_ptr() + 8 * r * slot), cnt),
+                       "export")
+            ok(lib.GxB_Vector_bitmap_import(q, ctypes.c_void_p(staged.data_ptr()), words), "import")
+        else:
+            with torch.cuda.stream(stream):
+                qb = gdev.device_tensor(torch, gdev.vector_view(q).bitmap, words)
+                for r, p in enumerate(parts):
+                    cnt = p["hi_w"] - p["lo_w"]
+                    if cnt:
+                        qb[p["lo_w"]:p["hi_w"]].copy_(gdev.device_tensor(torch, gdev.vector_view(ql[r]).bitmap, cnt))
+            ok(lib.GxB_Vector_device_touch(q), "touch")
+        t = ctypes.c_uint64()
+        ok(lib.GxB_Vector_publish_ticket(ctypes.byref(t), q), "ticket")
+        assert t.value > 0
+        return q, t.value
+
+    rng = np.random.default_rng(scale + 10 * world)
+    for src in [int(np.argmax(deg)), int(rng.choice(np.flatnonzero(deg > 0)))]:
+        for x in v + ql:
+            ok(lib.GrB_Vector_clear(x), "clear")
+        for r, p in enumerate(parts):
+            if p["lo"] <= src < p["hi"]:
+                ok(lib.GrB_Vector_setElement_BOOL(ql[r], True, src - p["lo"]), "root")
+        gather_into(bufs[0], True)
+        first = {1: True}
+        issued = []
+
+        def enqueue(d):
+            issued.append(d)
+            for r, p in enumerate(parts):
+                ok(lib.GrB_Vector_assign_INT32(v[r], ql[r], None, d, lib.GrB_ALL, p["hi"] - p["lo"], None), "assign")
+            for r in range(world):
+                ok(lib.GrB_mxv(ql[r], v[r], None, sr, AT[r], bufs[(d - 1) % 2], lib.GrB_DESC_RSC), "mxv")
+            return gather_into(bufs[d % 2], first.pop(d % 2, False))
+
+        def count_of(tok):
+            c = ctypes.c_uint64()
+            ok(lib.GxB_Vector_wait_ticket(ctypes.byref(c), tok[0], ctypes.c_uint64(tok[1])), "wait ticket")
+            return c.value
+
+        nlev = gdist.pipelined_levels(enqueue, count_of, max_levels=n + 2)
+        got = np.zeros(n, np.int32)
+        for r, p in enumerate(parts):
+            idx, lv = _extract_int32(lib, v[r])
+            got[idx + p["lo"]] = lv
+        lev, _, _ = O.bfs_levels(G, src)
+        assert np.array_equal(got, lev), f"source {src}"
+        assert nlev == int(lev.max()) and issued == list(range(1, nlev + 2))
+        ok(lib.GrB_Vector_nvals(ctypes.byref(nv), bufs[nlev % 2]), "nvals")
+        assert nv.value == 0
+    # a ticket superseded by a later publish of the same vector is refused, never misread
+    t_old = gather_into(bufs[0], False)[1]
+    gather_into(bufs[0], False)
+    torch.cuda.synchronize()
+    c = ctypes.c_uint64()
+    assert lib.GxB_Vector_wait_ticket(ctypes.byref(c), bufs[0], ctypes.c_uint64(t_old)) == -3
+    for h in AT:
+        ok(lib.GrB_Matrix_free(ctypes.byref(h)), "free")
+    for h in v + ql + bufs:
+        ok(lib.GrB_Vector_free(ctypes.byref(h)), "free")
+
+
 @pytest.mark.parametrize("scale", [10, 13])
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("k", [7, 64])
