@@ -71,6 +71,32 @@ __device__ __forceinline__ bool dt_side_of(int64_t a, int64_t b) {
     return SWAP ? a > b : a >= b;
 }
 
+// a list side's values: full width, one iso value, or the cached narrow copy (gb_view_narrow:
+// integer values that all fit 1-4 bytes, widened on load -- a hit's value read then touches a
+// fraction of the cache lines)
+template <class X>
+struct dt_vals {
+    const X *v;
+    const void *nv;
+    int nk;
+    bool iso;
+    __device__ __forceinline__ X operator[](int64_t i) const {
+        if (iso) return v[0];
+        if constexpr (std::is_integral<X>::value && !std::is_same<X, bool>::value && sizeof(X) > 1) {
+            switch (nk) {
+            case 1: return (X)((const uint8_t *)nv)[i];
+            case -1: return (X)((const int8_t *)nv)[i];
+            case 2: if constexpr (sizeof(X) > 2) return (X)((const uint16_t *)nv)[i]; break;
+            case -2: if constexpr (sizeof(X) > 2) return (X)((const int16_t *)nv)[i]; break;
+            case 4: if constexpr (sizeof(X) > 4) return (X)((const uint32_t *)nv)[i]; break;
+            case -4: if constexpr (sizeof(X) > 4) return (X)((const int32_t *)nv)[i]; break;
+            default: break;
+            }
+        }
+        return v[i];
+    }
+};
+
 // ---------------------------------------------------------------- classify
 // flags (pre-zeroed): tflag[p] = 1 for this phase's entries of task-sized groups
 // (G order); entries whose longer list exceeds the cap: hg[p] = 1 (G order) when
@@ -335,12 +361,11 @@ __device__ __forceinline__ Z dt_mult(const SR &sr, X xv, X yv, int64_t g, int32_
 // Y's keys 64 at a time (|Y| <= |X|) and find each among X's keys by shuffles --
 // 6 steps over the lanes' first keys, then the KPL keys of the lane found.
 template <class SR, class X, class Z, bool SWAP, int KPL>
-__global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, dt_side s, const X *__restrict__ xvx, bool x_iso,
-                                                       const X *__restrict__ yvx, bool y_iso,
+__global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, dt_side s, dt_vals<X> xvx, dt_vals<X> yvx,
                                                        Z *__restrict__ tval, uint8_t *__restrict__ tflag) {
     const int lane = threadIdx.x & 63;
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    const bool rv = SR::reads_values && xvx && yvx;
+    const bool rv = SR::reads_values && xvx.v && yvx.v;
     constexpr int AMIN = KPL == 1 ? 1 : DT_SMALL + 1;
     for (int64_t g = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; g < s.ng; g += nw) {
         const int64_t xs = s.xrp[g];
@@ -354,7 +379,7 @@ __global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, dt_side s, const 
         // X's values held beside the keys (read by a shuffle on a hit, no dependent load)
         X xv[KPL];
 #pragma unroll
-        for (int j = 0; j < KPL; j++) xv[j] = (rv && lane * KPL + j < a) ? xvx[x_iso ? 0 : xs + lane * KPL + j] : X();
+        for (int j = 0; j < KPL; j++) xv[j] = (rv && lane * KPL + j < a) ? xvx[xs + lane * KPL + j] : X();
         for (int64_t pb = p0; pb < p1; pb += 64) {
             const int nb = __builtin_amdgcn_readfirstlane((int)std::min<int64_t>(64, p1 - pb));
             int32_t o_l = 0;
@@ -407,7 +432,7 @@ __global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, dt_side s, const 
                         }
                         if (pos >= 0) {
                             X yv = X();
-                            if (rv) yv = yvx[y_iso ? 0 : ys + f0 + lane];
+                            if (rv) yv = yvx[ys + f0 + lane];
                             const Z z = dt_mult<SR, X, Z, SWAP>(sr, xm, yv, g, yk, o);
                             acc = found ? sr.add(acc, z) : z;
                             found = true;
@@ -506,8 +531,7 @@ template <class SR, class X, class Z, bool SWAP>
 // 8 waves per SIMD: two workgroups per CU (round 3: one workgroup of 149.6 KB LDS and 78 VGPRs
 // per CU left the latency-bound stream at 4 waves per SIMD; s22 128 -> 117 ms, s20 27.2 -> 23.5)
 __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
-    SR sr, int mon, dt_side s, const X *__restrict__ xvx, bool x_iso, const X *__restrict__ yvx, bool y_iso,
-    int64_t ntask, const int64_t *__restrict__ tstart, const int32_t *__restrict__ eG,
+    SR sr, int mon, dt_side s, dt_vals<X> xvx, dt_vals<X> yvx, int64_t ntask, const int64_t *__restrict__ tstart, const int32_t *__restrict__ eG,
     const int64_t *__restrict__ eYS, const int32_t *__restrict__ eO, const int32_t *__restrict__ eB,
     const int64_t *__restrict__ eQ, Z *__restrict__ tval, uint8_t *__restrict__ tflag, int dbg,
     const uint16_t *__restrict__ ePc, int pcap, unsigned long long *__restrict__ tctr, int chunk) {
@@ -523,7 +547,7 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
     __shared__ int w_sum[DT_TB / 64];
     __shared__ int next_unit;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const bool rv = SR::reads_values && xvx && yvx;
+    const bool rv = SR::reads_values && xvx.v && yvx.v;
     // ANY (any_pair, or LOR over pair's 1s): the entry's value is any term -- store it;
     // every other monoid folds into its identity
     const bool ANY = std::is_same<SR, gb_sr_any_pair<Z>>::value || mon == GBAMD_MON_ANY;
@@ -679,8 +703,8 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
                     if (act && !(dbg & 1) && l < a && keys[l] == kk) {
                         X xv = X(), yv = X();
                         if (rv) {
-                            xv = xvx[x_iso ? 0 : xs + l];
-                            yv = yvx[y_iso ? 0 : p];
+                            xv = xvx[xs + l];
+                            yv = yvx[p];
                         }
                         const Z z = dt_mult<SR, X, Z, SWAP>(sr, xv, yv, g, kk, eO[e0 + e]);
                         if (e != cur_e) {  // a lane's staged elements come in entry order
@@ -791,16 +815,18 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
             } else {
                 sd = dt_side{mtrp, mtci, mperm, BT.nrows, BT.rowptr, BT.colidx, A.rowptr, A.colidx};
             }
-            const X *xv = (const X *)(SWAP ? btv : av);
-            const X *yv = (const X *)(SWAP ? av : btv);
-            const bool xiso = SWAP ? BT.iso : A.iso, yiso = SWAP ? A.iso : BT.iso;
+            // narrow copies apply when the kernels read the matrices' own values (no cast copy)
+            const dt_vals<X> va{(const X *)av, av == A.vals ? A.nvx : nullptr, av == A.vals ? A.nvk : 0, A.iso};
+            const dt_vals<X> vb{(const X *)btv, btv == BT.vals ? BT.nvx : nullptr, btv == BT.vals ? BT.nvk : 0,
+                                BT.iso};
+            const dt_vals<X> xv = SWAP ? vb : va, yv = SWAP ? va : vb;
             const unsigned gw = dt_grid(sd.ng * 64, DT_BLOCK, 1 << 15);
             hipLaunchKernelGGL((k_dot_small<SRT, X, Z, SWAP, 1>), dim3(gw), dim3(DT_BLOCK), 0, gb_stream(), srf, sd,
-                               xv, xiso, yv, yiso, (Z *)tval, tflag);
+                               xv, yv, (Z *)tval, tflag);
             const int64_t skip = gb_knob("dot_skip");  // diagnostics: 1 skips the mid kernel, 2 the task kernel
             if (!(skip & 1))
                 hipLaunchKernelGGL((k_dot_small<SRT, X, Z, SWAP, DT_MID / 64>), dim3(gw), dim3(DT_BLOCK), 0,
-                                   gb_stream(), srf, sd, xv, xiso, yv, yiso, (Z *)tval, tflag);
+                                   gb_stream(), srf, sd, xv, yv, (Z *)tval, tflag);
             // lists longer than the cap run as pieces of cap keys (4- and 8-byte results:
             // the pieces of an entry fold into its output slot with atomics)
             const bool pieces = (sizeof(Z) == 4 || sizeof(Z) == 8) && gb_knob("dot_pieces") != 1;
@@ -862,7 +888,7 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
                 if (chunk <= 0) chunk = 4;
                 if (!(skip & 2))
                     hipLaunchKernelGGL((k_dot_task<SRT, X, Z, SWAP>), dim3(gt), dim3(DT_TB), 0, gb_stream(), srf,
-                                       info.mon, sd, xv, xiso, yv, yiso, nt, tstart, eG, eYS, eO, eB, eQ, (Z *)tval,
+                                       info.mon, sd, xv, yv, nt, tstart, eG, eYS, eO, eB, eQ, (Z *)tval,
                                        tflag, (int)gb_knob("dot_dbg"), ePc, cap, tctr, (int)chunk);
                 GB_LAUNCH_CHECK();
             };

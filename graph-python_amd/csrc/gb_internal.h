@@ -111,6 +111,12 @@ struct GB_Matrix_opaque {
     int32_t *hot_ci[2];
     int32_t *hot_cols[2];
     int64_t hot_n[2];
+    // cached narrow copy of the integer values of the CSR (0) / CSC (1) orientation, when every
+    // value fits fewer bytes (gb_prim.hip gb_view_narrow): nar_k = 1/2/4 unsigned, -1/-2/-4
+    // signed bytes per value, 0 not narrowable; nar_done: computed
+    void *nar_vx[2];
+    int nar_k[2];
+    bool nar_done[2];
     // ---- bitmap (kind == VECTOR / SCALAR); length n = nrows (ncols == 1)
     uint64_t *bits;      // [ceil(n/64)]
     void *dense;         // [n] or [1] when iso
@@ -341,6 +347,8 @@ struct gb_csr_view {
     int64_t maxdeg = -1;                 // longest row (host; attached with the hub chunks, -1 unknown)
     const int32_t *lchunks = nullptr;    // long-row chunks (row, piece) of the general SpMV (when attached)
     int64_t nlchunks = -1;
+    const void *nvx = nullptr;           // narrow copy of vals (when attached; see GB_Obj::nar_vx)
+    int nvk = 0;                         // its kind: 1/2/4 unsigned, -1/-2/-4 signed bytes, 0 none
     const int32_t *hcolidx = nullptr;    // hot-column relabelled colidx (when attached; see GB_Obj::hot_ci)
     const int32_t *hcols = nullptr;      // the hot columns' original ids, rank order
     int64_t nhot = 0;
@@ -356,6 +364,9 @@ void gb_view_nonempty(gb_csr_view &v, GB_Obj *A, int orient);
 // rows of at most 4 entries without reading their bounds or edges
 void gb_view_pullfirst(gb_csr_view &v, GB_Obj *A, int orient, const int64_t *other_rowptr, int64_t other_n);
 void gb_view_long_rows(gb_csr_view &v, GB_Obj *A, int orient);
+// attach the cached narrow copy of matrix A's orientation's integer values (built on first use:
+// one min/max pass, then a cast) when they fit fewer bytes; v.nvx stays null otherwise
+void gb_view_narrow(gb_csr_view &v, GB_Obj *A, int orient);
 // attach (building on first use) the hot-column relabel of matrix A's orientation, when the
 // matrix is large enough for the x gathers of a dense-input SpMV to miss in L2
 void gb_view_hot(gb_csr_view &v, GB_Obj *A, int orient);

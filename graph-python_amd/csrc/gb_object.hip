@@ -141,6 +141,10 @@ void gb_drop_transpose(GB_Obj *A) {
         A->hot_cols[o] = nullptr;
         A->hot_n[o] = 0;
         A->long_n[o] = 0;
+        gb_free(A->nar_vx[o]);
+        A->nar_vx[o] = nullptr;
+        A->nar_k[o] = 0;
+        A->nar_done[o] = false;
     }
 }
 

@@ -170,6 +170,11 @@ static void do_mxm(GB_Obj *C, GB_Obj *M, GrB_BinaryOp accum, GrB_Semiring sr, GB
         if (d.tran1) gb_get_csr(btv, B);
         else gb_get_csc(btv, B);
         btp = &btv;
+        // the masked dot reads one value per matching key: narrow copies of integer values
+        if (gb_sr_describe(sr).reads_values) {
+            gb_view_narrow(av, A, d.tran0 ? 1 : 0);
+            gb_view_narrow(btv, B, d.tran1 ? 0 : 1);
+        }
     }
     gb_mat_result T;
     gb_spgemm(T, av, bv, btp, m, sr);

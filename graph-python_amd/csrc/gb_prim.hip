@@ -3,7 +3,10 @@
 // typecasts, bitmap <-> CSR conversion, CSR transpose.
 #include <hipcub/hipcub.hpp>
 
+#include <climits>
+
 #include "gb_device.cuh"
+#include "gb_dispatch.cuh"
 #include "gb_internal.h"
 
 #define GB_BLOCK 256
@@ -538,4 +541,124 @@ void gb_view_hot(gb_csr_view &v, GB_Obj *A, int orient) {
     v.hcolidx = A->hot_ci[orient];
     v.hcols = A->hot_cols[orient];
     v.nhot = A->hot_n[orient];
+}
+
+// ------------------------------------------------------------------ narrow values
+// Integer values that all fit fewer bytes are kept a second time in that width (exact: the
+// kernels widen on load), so a kernel whose value reads are scattered -- the masked dot's hits
+// read one value per matching key -- touches 2-8x fewer cache lines.  R-MAT's INT64 weights
+// (1..255) take one byte.  Built once per matrix version and orientation (dropped with the
+// transpose cache).
+template <class T>
+__global__ void k_minmax(const T *__restrict__ x, int64_t n, long long *__restrict__ mn,
+                         unsigned long long *__restrict__ mx_u, long long *__restrict__ mx_s) {
+    long long lmn = LLONG_MAX, lmx = LLONG_MIN;
+    unsigned long long umx = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const T v = x[i];
+        if constexpr (std::is_signed<T>::value) {
+            lmn = (long long)v < lmn ? (long long)v : lmn;
+            lmx = (long long)v > lmx ? (long long)v : lmx;
+        } else {
+            umx = (unsigned long long)v > umx ? (unsigned long long)v : umx;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const long long a = __shfl_xor(lmn, off, 64), b = __shfl_xor(lmx, off, 64);
+        const unsigned long long c = __shfl_xor(umx, off, 64);
+        lmn = a < lmn ? a : lmn;
+        lmx = b > lmx ? b : lmx;
+        umx = c > umx ? c : umx;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if constexpr (std::is_signed<T>::value) {
+            atomicMin(mn, lmn);
+            atomicMax(mx_s, lmx);
+        } else {
+            atomicMax(mx_u, umx);
+        }
+    }
+}
+
+template <class D, class T>
+__global__ void k_narrow(const T *__restrict__ x, int64_t n, D *__restrict__ y) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        y[i] = (D)x[i];
+}
+
+void gb_view_narrow(gb_csr_view &v, GB_Obj *A, int orient) {
+    v.nvx = nullptr;
+    v.nvk = 0;
+    if (A->kind != GB_KIND_MATRIX || v.iso || !v.vals || v.nvals == 0 || gb_knob("narrow") == 1) return;
+    const int code = v.tcode;
+    const bool sgn = code == GBAMD_T_INT16 || code == GBAMD_T_INT32 || code == GBAMD_T_INT64;
+    const bool uns = code == GBAMD_T_UINT16 || code == GBAMD_T_UINT32 || code == GBAMD_T_UINT64;
+    if (!sgn && !uns) return;
+    if (!A->nar_done[orient]) {
+        const size_t ts = gb_type_size(code);
+        gb_scratch s;
+        long long *st = s.get<long long>(3);
+        const long long init[3] = {LLONG_MAX, LLONG_MIN, 0};
+        gb_copy_h2d(st, init, sizeof(init));
+        unsigned g = gb_grid(v.nvals);
+        if (g > 4096) g = 4096;
+        gb_with_type(code, [&](auto z) {
+            using T = decltype(z);
+            if constexpr (std::is_integral<T>::value && sizeof(T) >= 2)
+                hipLaunchKernelGGL(k_minmax<T>, dim3(g), dim3(GB_BLOCK), 0, gb_stream(), (const T *)v.vals, v.nvals,
+                                   st, (unsigned long long *)(st + 2), st + 1);
+        });
+        GB_LAUNCH_CHECK();
+        long long h[3];
+        gb_copy_d2h(h, st, sizeof(h));
+        int k = 0;
+        auto fits = [&](int kk) -> bool {
+            if ((size_t)(kk < 0 ? -kk : kk) >= ts) return false;
+            if (uns) {
+                const unsigned long long mx = (unsigned long long)h[2];
+                return kk > 0 && mx <= (kk == 1 ? 0xffULL : kk == 2 ? 0xffffULL : 0xffffffffULL);
+            }
+            const long long mn = h[0], mx = h[1];
+            if (kk == 1) return mn >= 0 && mx <= 0xff;
+            if (kk == -1) return mn >= -128 && mx <= 127;
+            if (kk == 2) return mn >= 0 && mx <= 0xffff;
+            if (kk == -2) return mn >= -32768 && mx <= 32767;
+            if (kk == 4) return mn >= 0 && mx <= 0xffffffffLL;
+            return mn >= INT32_MIN && mx <= INT32_MAX;
+        };
+        for (int kk : {1, -1, 2, -2, 4, -4})
+            if (fits(kk)) {
+                k = kk;
+                break;
+            }
+        void *nv = nullptr;
+        if (k) {
+            const int nb = k < 0 ? -k : k;
+            nv = gb_malloc((size_t)v.nvals * nb);
+            gb_with_type(code, [&](auto z) {
+                using T = decltype(z);
+                if constexpr (std::is_integral<T>::value && sizeof(T) >= 2) {
+                    auto go = [&](auto d) {
+                        using D = decltype(d);
+                        hipLaunchKernelGGL((k_narrow<D, T>), dim3(g), dim3(GB_BLOCK), 0, gb_stream(),
+                                           (const T *)v.vals, v.nvals, (D *)nv);
+                    };
+                    switch (k) {
+                    case 1: go(uint8_t()); break;
+                    case -1: go(int8_t()); break;
+                    case 2: go(uint16_t()); break;
+                    case -2: go(int16_t()); break;
+                    case 4: go(uint32_t()); break;
+                    default: go(int32_t()); break;
+                    }
+                }
+            });
+            GB_LAUNCH_CHECK();
+        }
+        A->nar_vx[orient] = nv;
+        A->nar_k[orient] = k;
+        A->nar_done[orient] = true;
+    }
+    v.nvx = A->nar_vx[orient];
+    v.nvk = A->nar_vx[orient] ? A->nar_k[orient] : 0;
 }

@@ -934,3 +934,31 @@ def test_spmv_hot_columns_vs_oracle(gb, name, mon, mul, dt, hot):
                                            atol=1e-3 if dt == "FP32" else 1e-10)
             else:
                 assert np.array_equal(gv, ref.values), kind
+
+
+@pytest.mark.parametrize("lo,hi,dt", [(1, 256, "INT64"), (-128, 128, "INT64"), (0, 65536, "INT64"),
+                                      (-32768, 32768, "INT32"), (0, 1 << 32, "UINT64"), (-(1 << 31), 1 << 31, "INT64"),
+                                      (0, 1 << 40, "INT64"), (0, 60000, "UINT32")])
+def test_masked_dot_narrow_values(gb, lo, hi, dt):
+    """The masked dot reads hit values from a cached narrow copy when every integer value fits
+    1 / 2 / 4 bytes (gb_prim.hip gb_view_narrow; unsigned and signed kinds, and a range that fits
+    none).  C<A.S> = A min.+ A and plus.times, bit-exact vs the oracle and vs knob narrow = 1."""
+    rng = np.random.default_rng(abs(lo) + hi % 1000 + len(dt))
+    n = 1500
+    S = _skewed_both(rng, n, "BOOL")
+    r, c, _ = S.to_coo()
+    v = rng.integers(lo, hi, r.size, dtype=np.int64).astype(O.NP[dt])
+    Ao = O.Csr.from_coo(r, c, v, nrows=n, ncols=n, dtype=dt)
+    for name, mon, mul in (("min_plus", "MIN", "PLUS"), ("plus_times", "PLUS", "TIMES")):
+        sr = getattr(gb.semiring, name)[dt]
+        ref = O.mxm(O.Csr.empty(n, n, dt), Ao, Ao, (mon, mul, dt), mask=Ao, mask_struct=True)
+        got = []
+        for narrow in (0, 1):
+            gb.set_knob("narrow", narrow)
+            try:
+                Ag = _to_gb(gb, Ao)  # a fresh matrix: no narrow copy cached yet
+                got.append(Ag.mxm(Ag, sr).new(mask=Ag.S))
+            finally:
+                gb.set_knob("narrow", 0)
+        for Cg in got:
+            _check_mat(Cg, ref)
