@@ -584,13 +584,29 @@ struct win_sweep_lds {
     int64_t wsum[HG / 64];
 };
 
+// Window index of the long B rows (numeric pass, round 5): for each B row longer than
+// WIX_MIN entries, the positions where its columns cross the multiples of the window width
+// 2^lw (pos[slot * (nw + 1) + t] = first position with column >= t * 2^lw, t = 0..nw).  A
+// window end then costs one load (the row's index line, L2-resident across the row's sweeps)
+// instead of a cooperative search over the rest of the B row -- round 4's numeric pass moved
+// 12x the symbolic pass's bytes (profiles/r04_config5_s20_pmc.json), most of it those probes,
+// repeated for every (A entry, window, value group) of a row; a value group's end inside a
+// window is searched within the window's slice of the row only.
+constexpr int WIX_MIN = 64;
+struct win_index {
+    const int32_t *slot = nullptr;  // [B rows] slot of the row's index, -1: short row (searched)
+    const int64_t *pos = nullptr;
+    int lw = 0, nw = 0;
+};
+
 // Entries [g, g + ne): the end of range, lb(cend) in B(k,:), by a cooperative search --
 // 2^lg lanes per entry (as many as HG / ne allows, at most a wave) probe evenly spaced
 // positions, so a row of few entries with long (hub) B rows takes log_{2^lg}(length)
 // dependent loads instead of a per-thread gallop's ~2 log2(distance).
 __device__ __forceinline__ void win_entries(win_sweep_lds &L, int64_t g, int ne, int64_t cend,
                                             const int64_t *__restrict__ cur, const int32_t *__restrict__ aci,
-                                            const int64_t *__restrict__ brp, const int32_t *__restrict__ bci) {
+                                            const int64_t *__restrict__ brp, const int32_t *__restrict__ bci,
+                                            const win_index &wx = win_index{}) {
     constexpr int NEW = WEG / 64;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     if (tid < ne) {
@@ -614,7 +630,24 @@ __device__ __forceinline__ void win_entries(win_sweep_lds &L, int64_t g, int ne,
     if (act) {
         a = L.lo[e];
         b = a + L.rem[e];
-        if (cend > 0x7fffffff) a = b;  // the whole rest of the row
+        if (cend > 0x7fffffff) {
+            a = b;  // the whole rest of the row
+        } else if (wx.slot && q == 0) {
+            const int32_t sl = wx.slot[L.k[e]];
+            if (sl >= 0) {  // narrow [a, b) to the window slice holding cend (exact at a window end)
+                const int64_t W = 1LL << wx.lw;
+                const int64_t t = (cend + W - 1) >> wx.lw;
+                const int64_t *ip = wx.pos + (int64_t)sl * (wx.nw + 1);
+                const int64_t hi = ip[t < wx.nw ? t : wx.nw];
+                b = hi < b ? hi : b;
+                if ((cend & (W - 1)) == 0) a = b > a ? b : a;
+                else if (t >= 1 && ip[t - 1] > a) a = ip[t - 1] < b ? ip[t - 1] : b;
+            }
+        }
+    }
+    if (wx.slot) {  // the group's other lanes take lane q == 0's narrowed bracket
+        a = __shfl(a, gsh, 64);
+        b = __shfl(b, gsh, 64);
     }
     while (__ballot(a < b)) {
         const bool open = a < b;
@@ -702,11 +735,12 @@ template <class F>
 __device__ __forceinline__ int32_t win_sweep(win_sweep_lds &L, int64_t a0, int64_t a1, int32_t c0, int64_t cend,
                                              bool advance, int64_t *__restrict__ cur,
                                              const int32_t *__restrict__ aci, const int64_t *__restrict__ brp,
-                                             const int32_t *__restrict__ bci, F &&f) {
+                                             const int32_t *__restrict__ bci, F &&f,
+                                             const win_index &wx = win_index{}) {
     int32_t mn = 0x7fffffff;
     for (int64_t g = a0; g < a1; g += WEG) {
         const int ne = a1 - g < WEG ? (int)(a1 - g) : WEG;
-        win_entries(L, g, ne, cend, cur, aci, brp, bci);
+        win_entries(L, g, ne, cend, cur, aci, brp, bci, wx);
         if (advance) {
             const int32_t m = win_advance(L, g, ne, cur, bci);
             mn = m < mn ? m : mn;
@@ -835,7 +869,7 @@ __global__ __launch_bounds__(HG, 8) void k_window_num(
     const X *__restrict__ avx, bool a_iso, const int64_t *__restrict__ brp, const int32_t *__restrict__ bci,
     const X *__restrict__ bvx, bool b_iso, int64_t ncols, const int64_t *__restrict__ crp,
     int32_t *__restrict__ cci, Z *__restrict__ cvx, const uint32_t *__restrict__ rowbits, int64_t nwrow,
-    const int32_t *__restrict__ bslot) {
+    const int32_t *__restrict__ bslot, win_index wx) {
     using S = slot_of<Z>;
     constexpr int NW = HG / 64, TILE = HG * WP;
     extern __shared__ __align__(16) char smem[];
@@ -885,7 +919,9 @@ __global__ __launch_bounds__(HG, 8) void k_window_num(
             cur[p] = b0;
             if (b0 < brp[k + 1]) nmin = bci[b0] < nmin ? bci[b0] : nmin;
         }
-        int32_t c0 = block_min(nmin) & ~31;
+        // with the window index, windows start at multiples of W (their ends are index entries)
+        const int32_t calign = wx.slot ? ~(W - 1) : ~31;
+        int32_t c0 = block_min(nmin) & calign;
         int64_t outpos = crp[i];
         // the row's presence bits from the symbolic pass (k_row_window), when it stored them
         const int32_t slot = rowbits ? bslot[i] : -1;
@@ -909,10 +945,10 @@ __global__ __launch_bounds__(HG, 8) void k_window_num(
             // value sweep over the whole window (one group, or C-resident)
             const bool one = !rb && a1 - a0 <= WEG;
             if (one) {
-                win_entries(L, a0, (int)(a1 - a0), c1, cur, aci, brp, bci);
+                win_entries(L, a0, (int)(a1 - a0), c1, cur, aci, brp, bci, wx);
                 win_tiles(L, a0, (int)(a1 - a0), c0, bci, presence);
             } else if (!rb) {
-                win_sweep(L, a0, a1, c0, c1, false, cur, aci, brp, bci, presence);
+                win_sweep(L, a0, a1, c0, c1, false, cur, aci, brp, bci, presence, wx);
             }
             __syncthreads();
             // exclusive popcount prefix per word (each thread a run of `per` words)
@@ -999,7 +1035,7 @@ __global__ __launch_bounds__(HG, 8) void k_window_num(
                     __syncthreads();
                     return win_advance(L, a0, (int)(a1 - a0), cur, bci);
                 }
-                return win_sweep(L, a0, a1, c0, cend, true, cur, aci, brp, bci, f);
+                return win_sweep(L, a0, a1, c0, cend, true, cur, aci, brp, bci, f, wx);
             };
             // value groups of < vcap entries, each a run of 256-column chunks
             const int NB = W >> 8;
@@ -1040,9 +1076,41 @@ __global__ __launch_bounds__(HG, 8) void k_window_num(
                 }
             }
             outpos += m;
-            c0 = block_min(mn) & ~31;
+            c0 = block_min(mn) & calign;
         }
         __syncthreads();
+    }
+}
+
+// window index (win_index above): flag the long rows, then per long row a wave fills its
+// nw + 1 crossing positions by binary searches
+__global__ void k_wix_flag(const int64_t *__restrict__ brp, int64_t n, uint8_t *__restrict__ flag) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+        flag[k] = brp[k + 1] - brp[k] > WIX_MIN ? 1 : 0;
+}
+
+__global__ void k_wix_fill(const int64_t *__restrict__ brp, const int32_t *__restrict__ bci, int64_t n, int lw, int nw,
+                           const uint8_t *__restrict__ flag, const int64_t *__restrict__ pos,
+                           int32_t *__restrict__ slot, int64_t *__restrict__ ix) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t k = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; k < n;
+         k += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+        if (!flag[k]) {
+            if (lane == 0) slot[k] = -1;
+            continue;
+        }
+        const int64_t sl = pos[k], rs = brp[k], re = brp[k + 1];
+        if (lane == 0) slot[k] = (int32_t)sl;
+        for (int t = lane; t <= nw; t += 64) {
+            const int64_t key = (int64_t)t << lw;
+            int64_t lo = rs, hi = re;
+            while (lo < hi) {
+                const int64_t m = (lo + hi) >> 1;
+                if ((int64_t)bci[m] < key) lo = m + 1;
+                else hi = m;
+            }
+            ix[sl * (nw + 1) + t] = lo;
+        }
     }
 }
 
@@ -1287,6 +1355,28 @@ void spgemm_hash_run(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, const gb_
             const int64_t kg = gb_knob("window_in_c_groups");
             const int in_c_groups = kg > 0 ? (int)kg : 8;  // tools/sweep_in_c.sh: 2 226 ms, 4 208, 8 204, never 206 (config 5)
             if constexpr (!SYM && VALS) {
+                // the long B rows' window index (knob window_index = 1: none; at most 1024 windows)
+                win_index wx;
+                gb_scratch xs;
+                const int64_t nwx = (ncols + (1LL << lw) - 1) >> lw;
+                if (gb_knob("window_index") != 1 && nwx <= 1024 && B.nrows > 0) {
+                    uint8_t *fl = xs.get<uint8_t>(B.nrows);
+                    int64_t *pos = xs.get<int64_t>(B.nrows + 1);
+                    int32_t *slot = xs.get<int32_t>(B.nrows);
+                    hipLaunchKernelGGL(k_wix_flag, dim3(hgrid(B.nrows, 256, 4096)), dim3(256), 0, gb_stream(),
+                                       B.rowptr, B.nrows, fl);
+                    GB_LAUNCH_CHECK();
+                    gb_exclusive_scan_u8(fl, pos, B.nrows);
+                    const int64_t nlong = gb_read_i64(pos + B.nrows);
+                    int64_t *ix = xs.get<int64_t>(std::max<int64_t>(1, nlong * (nwx + 1)));
+                    hipLaunchKernelGGL(k_wix_fill, dim3(hgrid(B.nrows * 64, 256, 8192)), dim3(256), 0, gb_stream(),
+                                       B.rowptr, B.colidx, B.nrows, lw, (int)nwx, fl, pos, slot, ix);
+                    GB_LAUNCH_CHECK();
+                    wx.slot = slot;
+                    wx.pos = ix;
+                    wx.lw = lw;
+                    wx.nw = (int)nwx;
+                }
                 auto win = [&](auto detc) {
                     constexpr bool D = decltype(detc)::value;
                     const size_t sh = (size_t)(1 << lw) / 4 + (size_t)vcap * sizeof(S) +
@@ -1295,7 +1385,7 @@ void spgemm_hash_run(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, const gb_
                     hipLaunchKernelGGL((k_window_num<D, SRT, X, Z>), dim3(hgrid(b.c[4], 1, 2048)), dim3(HG), sh,
                                        gb_stream(), srf, mon, rows + b.st[4], b.c[4], lw, vcap, in_c_groups, cur,
                                        A.rowptr, A.colidx, ax, A.iso, B.rowptr, B.colidx, bx, B.iso, ncols, crp,
-                                       wci, wvx, (const uint32_t *)rowbits, nwrow, (const int32_t *)bslot);
+                                       wci, wvx, (const uint32_t *)rowbits, nwrow, (const int32_t *)bslot, wx);
                 };
                 if constexpr (FP) {
                     if (det) win(std::true_type{});

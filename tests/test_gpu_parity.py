@@ -625,7 +625,7 @@ UNMASKED_SR = [s for s in SEMIRINGS if s[1] != "ANY"] + [("any_pair", "ANY", "PA
 
 
 @pytest.mark.parametrize("name,mon,mul,dt", UNMASKED_SR)
-@pytest.mark.parametrize("method", ["hash", "hash_window", "hash_window_c"])
+@pytest.mark.parametrize("method", ["hash", "hash_window", "hash_window_c", "hash_window_lw10"])
 def test_hash_spgemm_rmat_vs_oracle(gb, name, mon, mul, dt, method):
     """Hash Gustavson on R-MAT s12 (rows in every bin: wave / workgroup LDS tables and, for
     the hub rows or with hash_window, the column-window kernel; hash_window_c shrinks the window's
@@ -641,7 +641,8 @@ def test_hash_spgemm_rmat_vs_oracle(gb, name, mon, mul, dt, method):
     A = _to_gb(gb, G)
     sr = getattr(gb.semiring, name)[dt]
     with _knobs(gb, hash_window=int(method != "hash"), window_vcap=512 if method == "hash_window_c" else 0,
-                window_in_c_groups=1 if method == "hash_window_c" else 0):
+                window_in_c_groups=1 if method == "hash_window_c" else 0,
+                window_lw=10 if method == "hash_window_lw10" else 0):
         C = A.mxm(A, sr).new()
     ref = O.mxm(O.Csr.empty(G.nrows, G.ncols, dt), G, G, (mon, mul, dt))
     if mon == "ANY":

@@ -42,6 +42,11 @@ METHODS = {
     "window": {"hash_window": 1},  # every row through the column windows (LDS value groups)
     "window_sweep": {"hash_window": 1, "window_bits": 1},  # presence by a product sweep, not stored bitmaps
     "window_in_c": {"hash_window": 1, "window_vcap": 512, "window_in_c_groups": 1},
+    # 4 windows of 1024 columns: window ends from the long B rows' window index (round 5), value
+    # groups inside a window searched in the row's window slice; and the same without the index
+    "window_lw10": {"hash_window": 1, "window_lw": 10},
+    "window_lw10_groups": {"hash_window": 1, "window_lw": 10, "window_vcap": 300},
+    "window_lw10_noindex": {"hash_window": 1, "window_lw": 10, "window_index": 1},
 }
 
 
