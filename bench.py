@@ -1163,8 +1163,9 @@ def main():
             if world < wmin:
                 continue
             key = "config5_spgemm_plus_times_fp64" + ("" if s5 == args.spgemm_scale else f"_s{s5}")
+            # a bounded CPU sample on both single-GPU lines (s19 and s20)
             secondary[key] = config5_spgemm(lib, torch, stream, O, dist, world, rank, args, s5,
-                                            cpu=s5 == args.spgemm_scale)
+                                            cpu=s5 in (args.spgemm_scale, args.spgemm_scale_big))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
