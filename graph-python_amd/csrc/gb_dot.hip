@@ -674,52 +674,104 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
 #pragma unroll
                 for (int u = 0; u < DT_U; u++) k_o[u] = s.yci[py[u]];
             };
-            for (int f0 = fu0; f0 < ((dbg & 8) ? fu0 : fu1); f0 += 64 * DT_U) {
-                int cnt = 0;
-                int32_t k[DT_U];
-                int ee[DT_U];
-                issue(f0, ee, k);
+            // one surviving element (its key passed the filter): binary search in X's keys; a hit
+            // loads the two values and folds into the lane's run (a lane's survivors come in
+            // element order, hence in entry order)
+            auto survivor = [&](bool act, int32_t kk, int f, int e) {
+                int l = 0;  // number of X keys < kk
+                for (int st = ksteps - 1; st >= 0; st--) {
+                    const int c = l + (1 << st);
+                    if (c <= a && keys[c - 1] < kk) l = c;
+                }
+                if (act && !(dbg & 1) && l < a && keys[l] == kk) {
+                    X xv = X(), yv = X();
+                    if (rv) {
+                        xv = xvx[xs + l];
+                        yv = yvx[e_ys[e] + (f - e_pre[e])];
+                    }
+                    const Z z = dt_mult<SR, X, Z, SWAP>(sr, xv, yv, g, kk, eO[e0 + e]);
+                    if (e != cur_e) {
+                        if (found) {
+                            dt_slot_fold(sr, ANY, &e_acc[cur_e], acc);
+                            atomicOr(&e_fnd[cur_e >> 5], 1u << (cur_e & 31));
+                        }
+                        cur_e = e;
+                        found = false;
+                    }
+                    acc = found ? sr.add(acc, z) : z;
+                    found = true;
+                }
+            };
+            if (dbg & 256) {
+                // diagnostics (A/B): round 4's survivors staged in LDS as (element, entry) and their
+                // keys loaded again from global memory before the search
+                for (int f0 = fu0; f0 < ((dbg & 8) ? fu0 : fu1); f0 += 64 * DT_U) {
+                    int cnt = 0;
+                    int32_t k[DT_U];
+                    int ee[DT_U];
+                    issue(f0, ee, k);
 #pragma unroll
-                for (int u = 0; u < DT_U; u++) {
-                    const int f = f0 + u * 64 + lane;
-                    const uint32_t h = dt_hash((dbg & 4) ? f : k[u]);
-                    const bool c = !(dbg & 2) && f < fu1 && ((filt[h >> 5] >> (h & 31)) & 1u);
-                    const unsigned long long m = __ballot(c);
-                    if (c) stg[cnt + __popcll(m & ltmask)] = f | (ee[u] << 17);
-                    cnt += __popcll(m);
-                }
-                gb_wave_sync();
-                for (int r = 0; r < cnt; r += 64) {
-                    const bool act = r + lane < cnt;
-                    const int w = act ? stg[r + lane] : 0;
-                    const int f = w & 0x1ffff, e = w >> 17;
-                    const int64_t p = act ? e_ys[e] + (f - e_pre[e]) : 0;
-                    const int32_t kk = act ? s.yci[p] : -1;
-                    int l = 0;  // number of X keys < kk
-                    for (int st = ksteps - 1; st >= 0; st--) {
-                        const int c = l + (1 << st);
-                        if (c <= a && keys[c - 1] < kk) l = c;
+                    for (int u = 0; u < DT_U; u++) {
+                        const int f = f0 + u * 64 + lane;
+                        const uint32_t h = dt_hash((dbg & 4) ? f : k[u]);
+                        const bool c = !(dbg & 2) && f < fu1 && ((filt[h >> 5] >> (h & 31)) & 1u);
+                        const unsigned long long m = __ballot(c);
+                        if (c) stg[cnt + __popcll(m & ltmask)] = f | (ee[u] << 17);
+                        cnt += __popcll(m);
                     }
-                    if (act && !(dbg & 1) && l < a && keys[l] == kk) {
-                        X xv = X(), yv = X();
-                        if (rv) {
-                            xv = xvx[xs + l];
-                            yv = yvx[p];
-                        }
-                        const Z z = dt_mult<SR, X, Z, SWAP>(sr, xv, yv, g, kk, eO[e0 + e]);
-                        if (e != cur_e) {  // a lane's staged elements come in entry order
-                            if (found) {
-                                dt_slot_fold(sr, ANY, &e_acc[cur_e], acc);
-                                atomicOr(&e_fnd[cur_e >> 5], 1u << (cur_e & 31));
+                    gb_wave_sync();
+                    for (int r = 0; r < cnt; r += 64) {
+                        const bool act = r + lane < cnt;
+                        const int w = act ? stg[r + lane] : 0;
+                        const int f = w & 0x1ffff, e = w >> 17;
+                        const int64_t p = act ? e_ys[e] + (f - e_pre[e]) : 0;
+                        survivor(act, act ? s.yci[p] : -1, f, e);
+                    }
+                    gb_wave_sync();  // the stage is rewritten by the next step
+                }
+            } else {
+                // Survivors are compacted in registers: each window's passing keys and their
+                // (element | entry << 17) words are forward-permuted (ds_permute, no LDS storage)
+                // into lanes [pc, pc + n) of a 64-lane batch -- the other lanes' values go to the
+                // complement, a permutation -- and a batch is searched only when full or at the
+                // unit's end.  Round 4 staged them in LDS and loaded each key again from global
+                // memory before its search, one partly filled round per step.  The step's filter
+                // words are read together (all DT_U reads in flight).
+                int32_t pk = -1;  // the batch: key and element|entry word per lane
+                int pm = 0, pc = 0;
+                for (int f0 = fu0; f0 < ((dbg & 8) ? fu0 : fu1); f0 += 64 * DT_U) {
+                    int32_t k[DT_U];
+                    int ee[DT_U];
+                    issue(f0, ee, k);
+                    uint32_t hh[DT_U], fw[DT_U];
+#pragma unroll
+                    for (int u = 0; u < DT_U; u++) hh[u] = dt_hash((dbg & 4) ? f0 + u * 64 + lane : k[u]);
+#pragma unroll
+                    for (int u = 0; u < DT_U; u++) fw[u] = filt[hh[u] >> 5];
+#pragma unroll
+                    for (int u = 0; u < DT_U; u++) {
+                        const int f = f0 + u * 64 + lane;
+                        const bool c = !(dbg & 2) && f < fu1 && ((fw[u] >> (hh[u] & 31)) & 1u);
+                        const unsigned long long m = __ballot(c);
+                        const int n = __popcll(m);
+                        if (n) {
+                            if (pc + n > 64) {  // batch full: search it first
+                                survivor(lane < pc, pk, pm & 0x1ffff, pm >> 17);
+                                pc = 0;
                             }
-                            cur_e = e;
-                            found = false;
+                            const int sr_ = __popcll(m & ltmask);
+                            const int dst = c ? pc + sr_ : (pc + n + (lane - sr_)) & 63;
+                            const int nk = __builtin_amdgcn_ds_permute(dst << 2, k[u]);
+                            const int nm = __builtin_amdgcn_ds_permute(dst << 2, f | (ee[u] << 17));
+                            if (lane >= pc && lane < pc + n) {
+                                pk = nk;
+                                pm = nm;
+                            }
+                            pc += n;
                         }
-                        acc = found ? sr.add(acc, z) : z;
-                        found = true;
                     }
                 }
-                gb_wave_sync();  // the stage is rewritten by the next step
+                if (pc) survivor(lane < pc, pk, pm & 0x1ffff, pm >> 17);
             }
             // end of the unit: one fold per wave when every lane's run is one entry
             const unsigned long long fb = __ballot(found);
