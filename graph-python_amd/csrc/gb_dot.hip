@@ -103,12 +103,14 @@ struct dt_vals {
 // they run as pieces, else hflag[q] = 1 (CSR order, the per-entry wave kernel)
 template <bool SWAP>
 __global__ __launch_bounds__(DT_BLOCK) void k_dt_classify(dt_side s, int cap, uint8_t *__restrict__ tflag,
-                                                         uint8_t *__restrict__ hflag, uint8_t *__restrict__ hg) {
+                                                         uint8_t *__restrict__ hflag, uint8_t *__restrict__ hg,
+                                                         bool hubs_chunked) {
     const int lane = threadIdx.x & 63;
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
     for (int64_t g = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; g < s.ng; g += nw) {
         const int64_t a = s.xrp[g + 1] - s.xrp[g];
         if (a <= DT_MID) continue;  // k_dot_small (or nothing to match)
+        if (hubs_chunked && a > cap) continue;  // k_dt_hub_classify
         for (int64_t p = s.grp_rp[g] + lane; p < s.grp_rp[g + 1]; p += 64) {
             const int32_t o = s.grp_oi[p];
             const int64_t b = s.yrp[o + 1] - s.yrp[o];
@@ -148,6 +150,77 @@ __global__ __launch_bounds__(DT_BLOCK) void k_dt_compact(dt_side s, int cap, con
     }
 }
 
+// Hub groups (longer list X(g,:) above the cap) hold most of the entries of a few groups --
+// an R-MAT hub row's group has up to ~10^5 entries -- so a wave per group leaves their entries
+// to a handful of waves (round 4: the hub compaction took 1.8-2.2 ms per phase, latency-bound
+// on those waves).  They are classified and compacted in chunks of DT_HCH entries instead, a
+// workgroup per chunk: k_dt_hub_count sizes the chunks per group (0 for other groups), a scan
+// numbers them, and the chunk kernels find their group by a binary search over that scan.
+constexpr int DT_HCH = 2048;
+
+__global__ void k_dt_hub_count(dt_side s, int cap, int32_t *__restrict__ nch, unsigned long long *__restrict__ amax) {
+    for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < s.ng; g += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t a = s.xrp[g + 1] - s.xrp[g], ne = s.grp_rp[g + 1] - s.grp_rp[g];
+        const bool hub = a > cap && ne > 0;
+        nch[g] = hub ? (int32_t)((ne + DT_HCH - 1) / DT_HCH) : 0;
+        if (hub) atomicMax(amax, (unsigned long long)a);
+    }
+}
+
+__device__ __forceinline__ int64_t dt_chunk_group(const int64_t *__restrict__ cp, int64_t ng, int64_t c) {
+    int64_t lo = 0, hi = ng;  // last g with cp[g] <= c
+    while (hi - lo > 1) {
+        const int64_t m = (lo + hi) >> 1;
+        if (cp[m] <= c) lo = m;
+        else hi = m;
+    }
+    return lo;
+}
+
+// flags of the hub groups' entries: hg[p] = 1 (G order) when they run as pieces, else hflag[q] = 1
+template <bool SWAP>
+__global__ __launch_bounds__(DT_BLOCK) void k_dt_hub_classify(dt_side s, const int64_t *__restrict__ cp,
+                                                             int64_t nchunk, uint8_t *__restrict__ hflag,
+                                                             uint8_t *__restrict__ hg) {
+    for (int64_t c = blockIdx.x; c < nchunk; c += gridDim.x) {
+        const int64_t g = dt_chunk_group(cp, s.ng, c);
+        const int64_t a = s.xrp[g + 1] - s.xrp[g];
+        const int64_t p0 = s.grp_rp[g] + (c - cp[g]) * DT_HCH, pe = s.grp_rp[g + 1];
+        const int64_t p1 = p0 + DT_HCH < pe ? p0 + DT_HCH : pe;
+        for (int64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+            const int32_t o = s.grp_oi[p];
+            const int64_t b = s.yrp[o + 1] - s.yrp[o];
+            if (b == 0 || !dt_side_of<SWAP>(a, b)) continue;
+            if (hg) hg[p] = 1;
+            else hflag[s.perm ? s.perm[p] : p] = 1;
+        }
+    }
+}
+
+template <bool SWAP>
+__global__ __launch_bounds__(DT_BLOCK) void k_dt_hub_compact(dt_side s, const int64_t *__restrict__ cp,
+                                                            int64_t nchunk, const uint8_t *__restrict__ hg,
+                                                            const int64_t *__restrict__ pos, int32_t *__restrict__ eG,
+                                                            int64_t *__restrict__ eYS, int32_t *__restrict__ eO,
+                                                            int32_t *__restrict__ eB, int64_t *__restrict__ eQ) {
+    for (int64_t c = blockIdx.x; c < nchunk; c += gridDim.x) {
+        const int64_t g = dt_chunk_group(cp, s.ng, c);
+        const int64_t p0 = s.grp_rp[g] + (c - cp[g]) * DT_HCH, pe = s.grp_rp[g + 1];
+        const int64_t p1 = p0 + DT_HCH < pe ? p0 + DT_HCH : pe;
+        for (int64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+            if (!hg[p]) continue;
+            const int32_t o = s.grp_oi[p];
+            const int64_t e = pos[p];
+            const int64_t ys = s.yrp[o];
+            eG[e] = (int32_t)g;
+            eYS[e] = ys;
+            eO[e] = o;
+            eB[e] = (int32_t)(s.yrp[o + 1] - ys);
+            eQ[e] = s.perm ? s.perm[p] : p;
+        }
+    }
+}
+
 // Pieces of the longest lists (> cap keys): piece j of X(g,:) is its keys
 // [j * cap, (j + 1) * cap).  An entry's work in piece j is the run of its Y keys
 // inside the piece's key range (found by two binary searches), cut into sub-entries
@@ -167,24 +240,12 @@ __device__ __forceinline__ int64_t dt_lower(const int32_t *__restrict__ v, int64
 // counts -- so a group's entries of one piece are consecutive (its tasks share that piece's
 // keys in LDS) and the pair space is exactly the pieces the entries have (the
 // round-4 piece-major layout was nh x the longest list's piece count).
-__device__ __forceinline__ void dt_group_span(const int32_t *__restrict__ hG, int64_t nh, int64_t i, int64_t &h0,
-                                              int64_t &h1) {
-    const int32_t g = hG[i];
-    int64_t lo = 0, hi = i;  // first index with hG == g
-    while (lo < hi) {
-        const int64_t m = (lo + hi) >> 1;
-        if (hG[m] < g) lo = m + 1;
-        else hi = m;
-    }
-    h0 = lo;
-    lo = i + 1;
-    hi = nh;  // first index with hG > g
-    while (lo < hi) {
-        const int64_t m = (lo + hi) >> 1;
-        if (hG[m] <= g) lo = m + 1;
-        else hi = m;
-    }
-    h1 = lo;
+// The span comes from the hub flags' exclusive scan `pos` (hub entry numbers in G order) at the
+// group's entry bounds: two loads (a binary search over hG cost 44 dependent loads per entry).
+__device__ __forceinline__ void dt_group_span(const dt_side &s, const int64_t *__restrict__ pos, int64_t g,
+                                              int64_t &h0, int64_t &h1) {
+    h0 = pos[s.grp_rp[g]];
+    h1 = pos[s.grp_rp[g + 1]];
 }
 
 __global__ void k_dt_piece_count(dt_side s, int64_t nh, int cap, const int32_t *__restrict__ hG,
@@ -195,46 +256,77 @@ __global__ void k_dt_piece_count(dt_side s, int64_t nh, int cap, const int32_t *
     }
 }
 
-// per pair: the entry's run of Y keys inside the piece's key range (two binary searches; the
-// runs of consecutive pieces follow each other, so each search starts where the last ended),
-// cut into sub-entries of at most cap keys (the task kernel's flat-space bound)
+// per pair: the entry's run of Y keys inside the piece's key range, cut into sub-entries of at
+// most cap keys (the task kernel's flat-space bound).  All of an entry's searches run in
+// lockstep -- the branchless lower bound's length sequence depends only on the Y list's length,
+// so up to 2 * DT_PB searches of a batch of pieces advance together with their loads in flight
+// (round 4 ran them one after another: 2 * pieces * log2(|Y|) dependent loads per entry)
+constexpr int DT_PB = 4;
+
 __global__ void k_dt_piece_flags(dt_side s, int64_t nh, int cap, const int32_t *__restrict__ hG,
                                  const int64_t *__restrict__ hYS, const int32_t *__restrict__ hB,
-                                 const int64_t *__restrict__ P, int32_t *__restrict__ cnt, int64_t *__restrict__ pys,
-                                 int32_t *__restrict__ pb) {
+                                 const int64_t *__restrict__ P, const int64_t *__restrict__ hpos,
+                                 int32_t *__restrict__ cnt, int64_t *__restrict__ pys, int32_t *__restrict__ pb) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nh; i += (int64_t)gridDim.x * blockDim.x) {
-        int64_t h0, h1;
-        dt_group_span(hG, nh, i, h0, h1);
         const int64_t g = hG[i], xs = s.xrp[g], a = s.xrp[g + 1] - xs;
+        int64_t h0, h1;
+        dt_group_span(s, hpos, g, h0, h1);
         const int64_t base = P[h0] + (i - h0), m = h1 - h0, np = P[i + 1] - P[i];
-        const int64_t ye = hYS[i] + hB[i];
-        int64_t lo = hYS[i];
-        for (int64_t j = 0; j < np; j++) {
-            const int64_t x0 = j * cap, x1 = (x0 + cap < a ? x0 + cap : a) - 1;
-            const int32_t k0 = s.xci[xs + x0], k1 = s.xci[xs + x1];
-            lo = dt_lower(s.yci, lo, ye, k0);
-            const int64_t hi = k1 == INT32_MAX ? ye : dt_lower(s.yci, lo, ye, k1 + 1);
-            const int64_t q = base + j * m;
-            pys[q] = lo;
-            pb[q] = (int32_t)(hi - lo);
-            cnt[q] = (int32_t)((hi - lo + cap - 1) / cap);
-            lo = hi;
+        const int64_t ys = hYS[i], ye = ys + hB[i];
+        for (int64_t j0 = 0; j0 < np; j0 += DT_PB) {
+            int32_t key[2 * DT_PB];
+            int64_t bp[2 * DT_PB];
+#pragma unroll
+            for (int u = 0; u < DT_PB; u++) {
+                const int64_t j = j0 + u < np ? j0 + u : np - 1;
+                const int64_t x0 = j * cap, x1 = (x0 + cap < a ? x0 + cap : a) - 1;
+                key[2 * u] = s.xci[xs + x0];
+                const int32_t k1 = s.xci[xs + x1];
+                key[2 * u + 1] = k1 == INT32_MAX ? INT32_MAX : k1 + 1;  // INT32_MAX: search to the end
+                bp[2 * u] = bp[2 * u + 1] = ys;
+            }
+            int64_t n = ye - ys;
+            while (n > 1) {
+                const int64_t half = n >> 1;
+#pragma unroll
+                for (int q = 0; q < 2 * DT_PB; q++)
+                    if (s.yci[bp[q] + half - 1] < key[q]) bp[q] += half;
+                n -= half;
+            }
+            int64_t lb[2 * DT_PB];
+#pragma unroll
+            for (int q = 0; q < 2 * DT_PB; q++) {
+                // bp is the last candidate: the lower bound is bp or bp + 1
+                lb[q] = (n == 1 && s.yci[bp[q]] < key[q]) ? bp[q] + 1 : bp[q];
+                if ((q & 1) && key[q] == INT32_MAX) lb[q] = ye;
+            }
+#pragma unroll
+            for (int u = 0; u < DT_PB; u++) {
+                const int64_t j = j0 + u;
+                if (j >= np) break;
+                const int64_t lo = lb[2 * u], hi = lb[2 * u + 1] > lo ? lb[2 * u + 1] : lo;
+                const int64_t q = base + j * m;
+                pys[q] = lo;
+                pb[q] = (int32_t)(hi - lo);
+                cnt[q] = (int32_t)((hi - lo + cap - 1) / cap);
+            }
         }
     }
 }
 
 // every pair's sub-entries at its scanned position; ePc[e] = the piece
-__global__ void k_dt_piece_compact(int64_t nh, int cap, const int32_t *__restrict__ hG, const int32_t *__restrict__ hO,
-                                   const int64_t *__restrict__ hQ, const int64_t *__restrict__ P,
+__global__ void k_dt_piece_compact(dt_side s, int64_t nh, int cap, const int32_t *__restrict__ hG,
+                                   const int32_t *__restrict__ hO, const int64_t *__restrict__ hQ,
+                                   const int64_t *__restrict__ P, const int64_t *__restrict__ hpos,
                                    const int32_t *__restrict__ cnt, const int64_t *__restrict__ ppos,
                                    const int64_t *__restrict__ pys, const int32_t *__restrict__ pb,
                                    int32_t *__restrict__ eG, int64_t *__restrict__ eYS, int32_t *__restrict__ eO,
                                    int32_t *__restrict__ eB, int64_t *__restrict__ eQ, uint16_t *__restrict__ ePc) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nh; i += (int64_t)gridDim.x * blockDim.x) {
-        int64_t h0, h1;
-        dt_group_span(hG, nh, i, h0, h1);
-        const int64_t base = P[h0] + (i - h0), m = h1 - h0, np = P[i + 1] - P[i];
         const int32_t g = hG[i], o = hO[i];
+        int64_t h0, h1;
+        dt_group_span(s, hpos, g, h0, h1);
+        const int64_t base = P[h0] + (i - h0), m = h1 - h0, np = P[i + 1] - P[i];
         const int64_t qq = hQ[i];
         for (int64_t j = 0; j < np; j++) {
             const int64_t q = base + j * m;
@@ -300,6 +392,42 @@ __global__ void k_dt_task_fill(int64_t ne, const uint8_t *__restrict__ ts, const
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x)
         if (ts[e]) tstart[tpos[e]] = e;
     if (blockIdx.x == 0 && threadIdx.x == 0) tstart[tpos[ne]] = ne;
+}
+
+// one task's descriptor, built before the task kernel (k_dt_task_desc) so that a workgroup
+// starting a task issues one load instead of the tstart -> eG -> row-pointer chain of
+// dependent loads (round 5)
+struct dt_task {
+    int64_t e0;     // first entry (task order)
+    int64_t xs;     // X(g,:)'s (piece's) first key
+    int32_t ne;     // entries
+    int32_t g;      // group
+    int32_t a;      // X keys (of the piece)
+    int32_t piece;  // -1, or the piece of a list longer than the cap
+};
+
+__global__ void k_dt_task_desc(int64_t nt, const int64_t *__restrict__ tstart, const int32_t *__restrict__ eG,
+                               const uint16_t *__restrict__ ePc, const int64_t *__restrict__ xrp, int pcap,
+                               dt_task *__restrict__ td) {
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nt; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e0 = tstart[t];
+        const int32_t g = eG[e0];
+        const int piece = ePc ? (int)ePc[e0] : -1;
+        int64_t xs = xrp[g], alen = xrp[g + 1] - xs;
+        if (piece >= 0) {
+            xs += (int64_t)piece * pcap;
+            alen -= (int64_t)piece * pcap;
+            if (alen > pcap) alen = pcap;
+        }
+        dt_task d;
+        d.e0 = e0;
+        d.xs = xs;
+        d.ne = (int32_t)(tstart[t + 1] - e0);
+        d.g = g;
+        d.a = (int32_t)alen;
+        d.piece = piece;
+        td[t] = d;
+    }
 }
 
 __global__ void k_dt_positions(int64_t n, const uint8_t *__restrict__ flag, const int64_t *__restrict__ pos,
@@ -531,7 +659,7 @@ template <class SR, class X, class Z, bool SWAP>
 // 8 waves per SIMD: two workgroups per CU (round 3: one workgroup of 149.6 KB LDS and 78 VGPRs
 // per CU left the latency-bound stream at 4 waves per SIMD; s22 128 -> 117 ms, s20 27.2 -> 23.5)
 __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
-    SR sr, int mon, dt_side s, dt_vals<X> xvx, dt_vals<X> yvx, int64_t ntask, const int64_t *__restrict__ tstart, const int32_t *__restrict__ eG,
+    SR sr, int mon, dt_side s, dt_vals<X> xvx, dt_vals<X> yvx, int64_t ntask, const dt_task *__restrict__ tdesc, const int32_t *__restrict__ eG,
     const int64_t *__restrict__ eYS, const int32_t *__restrict__ eO, const int32_t *__restrict__ eB,
     const int64_t *__restrict__ eQ, Z *__restrict__ tval, uint8_t *__restrict__ tflag, int dbg,
     const uint16_t *__restrict__ ePc, int pcap, unsigned long long *__restrict__ tctr, int chunk) {
@@ -568,29 +696,35 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
     if (c0 >= ntask) break;
     const int64_t c1 = c0 + chunk < ntask ? c0 + chunk : ntask;
     for (int64_t t = c0; t < c1; t++) {
-        const int64_t e0 = tstart[t];
-        const int ne = __builtin_amdgcn_readfirstlane((int)(tstart[t + 1] - e0));
-        const int64_t g = eG[e0];
-        const int piece = ePc ? (int)ePc[e0] : -1;  // a piece of a list longer than the cap
+        const dt_task td = tdesc[t];  // one load (uniform)
+        const int64_t e0 = td.e0;
+        const int ne = __builtin_amdgcn_readfirstlane(td.ne);
+        const int64_t g = td.g;
+        const int piece = td.piece;  // a piece of a list longer than the cap
         const bool reuse = g == prev_g && piece == prev_pc && !(dbg & 64);  // dbg 64: reload X every task (A/B)
         prev_g = g;
         prev_pc = piece;
-        int64_t xs = s.xrp[g];
-        int64_t alen = s.xrp[g + 1] - xs;
-        if (piece >= 0) {
-            xs += (int64_t)piece * pcap;
-            alen -= (int64_t)piece * pcap;
-            if (alen > pcap) alen = pcap;
+        const int64_t xs = td.xs;
+        const int a = __builtin_amdgcn_readfirstlane(td.a);
+        // the entries' and X's loads issued together, before any LDS work (one round trip)
+        int b = 0;
+        int64_t ysv = 0;
+        if (tid < ne) {
+            b = eB[e0 + tid];
+            ysv = eYS[e0 + tid];
         }
-        const int a = __builtin_amdgcn_readfirstlane((int)alen);
+        constexpr int XPT = DT_CAP / DT_TB;  // X keys per thread
+        int32_t xk[XPT];
+        if (!reuse) {
+#pragma unroll
+            for (int j = 0; j < XPT; j++) xk[j] = tid + j * DT_TB < a ? s.xci[xs + tid + j * DT_TB] : 0;
+        }
         if (!reuse)
             for (int i = tid; i < (1 << (DT_FLOG - 5)); i += DT_TB) filt[i] = 0;
         for (int i = tid; i < DT_SMAX / 64 + 1; i += DT_TB) estart[i] = 0;
         for (int i = tid; i < DT_MAXE / 32; i += DT_TB) e_fnd[i] = 0;
-        int b = 0;
         if (tid < ne) {
-            b = eB[e0 + tid];
-            e_ys[tid] = eYS[e0 + tid];
+            e_ys[tid] = ysv;
             unsigned long long iv = 0;
             __builtin_memcpy(&iv, &ident, sizeof(Z));
             e_acc[tid] = iv;
@@ -604,13 +738,17 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
         if (lane == 63) w_sum[wid] = inc;
         if (tid == 0) next_unit = 0;
         __syncthreads();  // filter and start bits cleared, wave sums visible
-        if (!reuse)
-            for (int i = tid; i < a; i += DT_TB) {
-                const int32_t k = s.xci[xs + i];
-                keys[i] = k;
-                const uint32_t h = dt_hash(k);
-                atomicOr(&filt[h >> 5], 1u << (h & 31));
+        if (!reuse) {
+#pragma unroll
+            for (int j = 0; j < XPT; j++) {
+                if (tid + j * DT_TB < a) {
+                    const int32_t k = xk[j];
+                    keys[tid + j * DT_TB] = k;
+                    const uint32_t h = dt_hash(k);
+                    atomicOr(&filt[h >> 5], 1u << (h & 31));
+                }
             }
+        }
         int base = 0, S = 0;
         for (int w = 0; w < DT_TB / 64; w++) {
             if (w < wid) base += w_sum[w];
@@ -884,9 +1022,28 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
             const bool pieces = (sizeof(Z) == 4 || sizeof(Z) == 8) && gb_knob("dot_pieces") != 1;
             gb_memset(tf, 0, nm);
             if (pieces) gb_memset(hg, 0, nm);
+            // hub groups in chunks (knob dot_hubchunk = 1: a wave per hub group, as in round 4)
+            const bool hubc = gb_knob("dot_hubchunk") != 1;
             hipLaunchKernelGGL((k_dt_classify<SWAP>), dim3(gw), dim3(DT_BLOCK), 0, gb_stream(), sd, cap, tf, hflag,
-                               pieces ? hg : nullptr);
+                               pieces ? hg : nullptr, hubc);
             GB_LAUNCH_CHECK();
+            gb_scratch hcs;
+            int64_t *hcp = nullptr, nhch = 0;
+            unsigned long long *amax = hcs.get<unsigned long long>(1);
+            gb_memset(amax, 0, sizeof(unsigned long long));
+            if (hubc) {
+                int32_t *nch = hcs.get<int32_t>(sd.ng);
+                hcp = hcs.get<int64_t>(sd.ng + 1);
+                hipLaunchKernelGGL(k_dt_hub_count, dim3(dt_grid(sd.ng)), dim3(DT_BLOCK), 0, gb_stream(), sd, cap, nch,
+                                   amax);
+                GB_LAUNCH_CHECK();
+                gb_exclusive_scan_i32(nch, 0, hcp, sd.ng);
+                nhch = gb_read_i64(hcp + sd.ng);
+                if (nhch)
+                    hipLaunchKernelGGL((k_dt_hub_classify<SWAP>), dim3((unsigned)std::min<int64_t>(nhch, 1 << 16)),
+                                       dim3(DT_BLOCK), 0, gb_stream(), sd, hcp, nhch, hflag, pieces ? hg : nullptr);
+                GB_LAUNCH_CHECK();
+            }
             // tasks over (eG, eYS, eO, eB, eQ) in task order: cut at group changes and windows
             auto run_tasks = [&](int64_t ne, int32_t *eG, int64_t *eYS, int32_t *eO, int32_t *eB, int64_t *eQ,
                                  const uint16_t *ePc) {
@@ -930,6 +1087,10 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
                 hipLaunchKernelGGL(k_dt_task_fill, dim3(dt_grid(ne)), dim3(DT_BLOCK), 0, gb_stream(), ne, tsf, tpos,
                                    tstart);
                 GB_LAUNCH_CHECK();
+                dt_task *tdesc = ts.get<dt_task>(nt);
+                hipLaunchKernelGGL(k_dt_task_desc, dim3(dt_grid(nt)), dim3(DT_BLOCK), 0, gb_stream(), nt, tstart, eG,
+                                   ePc, sd.xrp, cap, tdesc);
+                GB_LAUNCH_CHECK();
                 // persistent workgroups (two per CU) taking chunks of consecutive tasks
                 const unsigned gt = (unsigned)std::min<int64_t>(nt, 1024);
                 unsigned long long *tctr = ts.get<unsigned long long>(1);
@@ -940,7 +1101,7 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
                 if (chunk <= 0) chunk = 4;
                 if (!(skip & 2))
                     hipLaunchKernelGGL((k_dot_task<SRT, X, Z, SWAP>), dim3(gt), dim3(DT_TB), 0, gb_stream(), srf,
-                                       info.mon, sd, xv, yv, nt, tstart, eG, eYS, eO, eB, eQ, (Z *)tval,
+                                       info.mon, sd, xv, yv, nt, tdesc, eG, eYS, eO, eB, eQ, (Z *)tval,
                                        tflag, (int)gb_knob("dot_dbg"), ePc, cap, tctr, (int)chunk);
                 GB_LAUNCH_CHECK();
             };
@@ -980,10 +1141,13 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
             int32_t *hO = hs.get<int32_t>(nh);
             int32_t *hB = hs.get<int32_t>(nh);
             int64_t *hQ = hs.get<int64_t>(nh);
-            unsigned long long *amax = hs.get<unsigned long long>(1);
-            gb_memset(amax, 0, sizeof(unsigned long long));
-            hipLaunchKernelGGL((k_dt_compact<SWAP>), dim3(gw), dim3(DT_BLOCK), 0, gb_stream(), sd, cap, hg, pos, hG,
-                               hYS, hO, hB, hQ, true, amax);
+            if (hubc) {
+                hipLaunchKernelGGL((k_dt_hub_compact<SWAP>), dim3((unsigned)std::min<int64_t>(nhch, 1 << 16)),
+                                   dim3(DT_BLOCK), 0, gb_stream(), sd, hcp, nhch, hg, pos, hG, hYS, hO, hB, hQ);
+            } else {
+                hipLaunchKernelGGL((k_dt_compact<SWAP>), dim3(gw), dim3(DT_BLOCK), 0, gb_stream(), sd, cap, hg, pos,
+                                   hG, hYS, hO, hB, hQ, true, amax);
+            }
             Z ident = Z();
             if (!(std::is_same<SRT, gb_sr_any_pair<Z>>::value || info.mon == GBAMD_MON_ANY))
                 ident = gb_monoid_identity<Z>(info.mon);
@@ -1016,7 +1180,7 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
             int64_t *pys = hs.get<int64_t>(npairs);
             int32_t *pb = hs.get<int32_t>(npairs);
             hipLaunchKernelGGL(k_dt_piece_flags, dim3(dt_grid(nh)), dim3(DT_BLOCK), 0, gb_stream(), sd, nh, cap, hG,
-                               hYS, hB, P, pc, pys, pb);
+                               hYS, hB, P, pos, pc, pys, pb);
             GB_LAUNCH_CHECK();
             gb_exclusive_scan_i32(pc, 0, ppos, npairs);
             const int64_t npe = gb_read_i64(ppos + npairs);
@@ -1028,8 +1192,8 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
             int32_t *eB = ps.get<int32_t>(npe);
             int64_t *eQ = ps.get<int64_t>(npe);
             uint16_t *ePc = ps.get<uint16_t>(npe);
-            hipLaunchKernelGGL(k_dt_piece_compact, dim3(dt_grid(nh)), dim3(DT_BLOCK), 0, gb_stream(), nh, cap, hG, hO,
-                               hQ, P, pc, ppos, pys, pb, eG, eYS, eO, eB, eQ, ePc);
+            hipLaunchKernelGGL(k_dt_piece_compact, dim3(dt_grid(nh)), dim3(DT_BLOCK), 0, gb_stream(), sd, nh, cap, hG,
+                               hO, hQ, P, pos, pc, ppos, pys, pb, eG, eYS, eO, eB, eQ, ePc);
             GB_LAUNCH_CHECK();
             run_tasks(npe, eG, eYS, eO, eB, eQ, ePc);
         };
