@@ -13,6 +13,7 @@
 #   stats:NAME            rocprofv3 --kernel-trace --stats of the default bench (no CPU baseline)
 #                         -> gpurun_out/NAME/ + top kernels (tools/kstats.py)
 #   prof:NAME:CMD         the same for CMD (comma-separated argv: a script under the repo root + args)
+#   roctx:NAME:CMD        kernel trace + roctx ranges per library call (tools/prof_roctx.sh)
 #   pmc:NAME:REGEX:CMD    tools/pmc_passes.sh NAME REGEX CMD (trace + FETCH / WRITE / TCC / SQ passes)
 #   pmck:NAME:REGEX:CMD   tools/pmc_kernel.sh NAME REGEX CMD (instruction mix, LDS, waits, L2, FETCH)
 #   py:CMD                python3 CMD (comma-separated argv), 300 s limit
@@ -63,6 +64,10 @@ for step in "$@"; do
     name=${rest%%:*}; cmd=${rest#*:}
     argv=(${cmd//,/ })
     bash tools/prof_cmd.sh "$name" python3 "$R/${argv[0]}" "${argv[@]:1}" || exit 1 ;;
+  roctx)
+    name=${rest%%:*}; cmd=${rest#*:}
+    argv=(${cmd//,/ })
+    bash tools/prof_roctx.sh "$name" python3 "$R/${argv[0]}" "${argv[@]:1}" || exit 1 ;;
   pmc)
     name=${rest%%:*}; r2=${rest#*:}; regex=${r2%%:*}; cmd=${r2#*:}
     argv=(${cmd//,/ })
