@@ -307,15 +307,18 @@ __device__ __forceinline__ void msplit(const int (&ow)[P], int (&pos)[P], int32_
     int rk[P];
 #pragma unroll
     for (int u = 0; u < P; u++) {
-        int mine = 0;
-        rk[u] = 0;
+        // the lanes sharing this lane's owner, from one ballot per bit of the owner number
+        // (lg2(NW) + 1 ballots; round 4 took one ballot per owner, NW of them)
+        unsigned long long same = ~0ULL;
 #pragma unroll
-        for (int o = 0; o < NW; o++) {
-            const unsigned long long m = __ballot(ow[u] == o);
-            if (lane == o) mine = __popcll(m);
-            if (ow[u] == o) rk[u] = __popcll(m & lt);
+        for (int b = 0; b <= lg2c<NW>::v; b++) {
+            const bool bit = (ow[u] >> b) & 1;
+            const unsigned long long bb = __ballot(bit);
+            same &= bit ? bb : ~bb;
         }
-        if (lane < NW) cnt[u][w][lane] = mine;
+        rk[u] = __popcll(same & lt);
+        if (lane < NW) cnt[u][w][lane] = 0;
+        if (ow[u] < NW && rk[u] == 0) cnt[u][w][ow[u]] = __popcll(same);  // after the zeros (same wave)
     }
     __syncthreads();
     const int uu = lane / NW, oo = lane % NW;

@@ -42,13 +42,24 @@ nv = ctypes.c_uint64()
 sr = lib.GxB_ANY_PAIR_BOOL if anypair else lib.GrB_LOR_LAND_SEMIRING_BOOL
 desc, ALL = lib.GrB_DESC_RSC, lib.GrB_ALL
 f_assign, f_vxm, f_nvals = lib.GrB_Vector_assign_INT32, lib.GrB_vxm, lib.GrB_Vector_nvals
-tot = {"assign": [], "vxm": [], "nvals": [], "loop": []}
+tot = {"assign": [], "vxm": [], "nvals": [], "loop": [], "start_clear_q": [], "start_clear_v": [],
+       "start_setElement": []}
 last = []
+sync_start = "nosync" not in sys.argv[2:]  # nosync: BFS after BFS as the bench runs them
 for rep in range(20):
+    s0 = time.perf_counter()
     lib.GrB_Vector_clear(q)
+    s1 = time.perf_counter()
     lib.GrB_Vector_clear(v)
+    s2 = time.perf_counter()
     lib.GrB_Vector_setElement_BOOL(q, True, 12345 + rep)
-    torch.cuda.synchronize()
+    s3 = time.perf_counter()
+    if rep >= 5:
+        tot["start_clear_q"].append(s1 - s0)
+        tot["start_clear_v"].append(s2 - s1)
+        tot["start_setElement"].append(s3 - s2)
+    if sync_start:
+        torch.cuda.synchronize()
     d = 0
     while True:
         d += 1
