@@ -713,15 +713,22 @@ __device__ __forceinline__ void win_tiles(const win_sweep_lds &L, int64_t g, int
         int sx[WP];
         int64_t pb[WP];
         bool ok[WP];
+        // a thread's WP products are consecutive in the flat order (round 5; round 4 strided them
+        // by HG): one binary search for the first, the next entry found by stepping forward
+        // (loads stay coalesced: a wave covers 64 * WP consecutive products)
+        int s = 0;
 #pragma unroll
         for (int u = 0; u < WP; u++) {
-            const int32_t t = t0 + tid + HG * u;
+            const int32_t t = t0 + tid * WP + u;
             ok[u] = t < G;
-            int s = 0;
             if (ok[u]) {
+                if (u == 0) {
 #pragma unroll
-                for (int st = top >> 1; st > 0; st >>= 1)
-                    if (s + st < ne && L.excl[s + st] <= t) s += st;
+                    for (int st = top >> 1; st > 0; st >>= 1)
+                        if (s + st < ne && L.excl[s + st] <= t) s += st;
+                } else {
+                    while (s + 1 < ne && L.excl[s + 1] <= t) s++;
+                }
             }
             sx[u] = s;
             pb[u] = ok[u] ? L.lo[s] + (t - L.excl[s]) : 0;
