@@ -654,7 +654,7 @@ __device__ __forceinline__ void win_entries(win_sweep_lds &L, int64_t g, int ne,
     }
     while (__ballot(a < b)) {
         const bool open = a < b;
-        const int64_t step = open ? (b - a + Lw - 1) / Lw : 1;
+        const int64_t step = open ? (b - a + Lw - 1) >> lg : 1;  // Lw = 2^lg: a shift, not a 64-bit division
         const int64_t pos = a + q * step;
         const bool pr = open && pos < b && bci[pos] < ce;
         const int t = __popcll((__ballot(pr) >> gsh) & gmask);
