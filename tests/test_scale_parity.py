@@ -12,7 +12,7 @@ checked here, through the C ABI exactly as bench.py drives them, against the CPU
   GrB_mxm on column words): every root's levels;
 * config 4: C<A.S> = A min.+ A (reference core/matrix.py:2241 via core/base.py:483), INT64,
   the whole C at s18 and 1024 sampled rows at s20, bit-exact vs O.mxm;
-* config 2: y = x plus.times A (GrB_vxm, dense fp64 x) at s20 and s22, ef 16, rtol 1e-6 vs
+* config 2: y = x plus.times A (GrB_vxm, dense fp64 x) at s20 and s22, ef 16 and 60, rtol 1e-6 vs
   scipy (BASELINE.json north_star's fp64 tolerance);
 * config 5: C = A plus.times A (unmasked hash Gustavson) at s19, 512 sampled rows (the 32
   longest rows first: the column-window bins) vs a numpy fold, rtol 1e-6.
@@ -204,14 +204,15 @@ def test_masked_min_plus_spgemm_bench_scale(gb, scale, rows):
     assert np.array_equal(Cs.values, ref.values)
 
 
-@pytest.mark.parametrize("scale", [20, 22])
-def test_spmv_plus_times_fp64_bench_scale(gb, scale):
-    """config 2's kernel: y = x plus.times A, dense fp64 x (hot-column relabel on by default)"""
+@pytest.mark.parametrize("scale,ef", [(20, 16), (22, 16), (22, 60)])
+def test_spmv_plus_times_fp64_bench_scale(gb, scale, ef):
+    """config 2's kernel: y = x plus.times A, dense fp64 x (hot-column relabel on by default); ef 60
+    is the com-Orkut entry count the bench's second config 2 line stands in for (235 M entries)"""
     import scipy.sparse as sp
 
     lib = gb.lib
     n = 1 << scale
-    A = rmat(lib, scale, "FP64")
+    A = rmat(lib, scale, "FP64", ef=ef)
     x, y = ctypes.c_void_p(), ctypes.c_void_p()
     xv = np.random.default_rng(1).random(n)
     idx = np.arange(n, dtype=np.uint64)
