@@ -60,7 +60,7 @@ def parse():
     p.add_argument("--no-msbfs-sharded", action="store_true",
                    help="N > 1: skip the row-sharded 64-root BFS line (one exchange per level for 64 roots)")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
-    p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r04.json"))
+    p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r05.json"))
     # rehearsal of the N>1 path on one GPU: all ranks on one device, gloo transport
     p.add_argument("--dist-backend", default="nccl")
     p.add_argument("--no-pipeline", action="store_true",
@@ -427,8 +427,9 @@ def config2_spmv(lib, torch, stream, args, scale, ef, O=None, cpu=False):
     parity2 = bool(np.array_equal(present, np.diff(S.tocsc().indptr) > 0) and
                    np.allclose(got, ref, rtol=1e-6, atol=1e-9))
     by = 12 * nnz + 8 * (n + 1) + 16 * n
-    traffic, src = _profile_traffic(*([f"r04_config2_s{sc}_pmc.json", f"r03_config2_s{sc}_pmc.json"] if ef == 16 else
-                                      [f"r04_config2_s{sc}_ef{ef}_pmc.json"]))
+    traffic, src = _profile_traffic(*([f"r05_config2_s{sc}_pmc.json", f"r04_config2_s{sc}_pmc.json",
+                                       f"r03_config2_s{sc}_pmc.json"] if ef == 16 else
+                                      [f"r05_config2_s{sc}_ef{ef}_pmc.json", f"r04_config2_s{sc}_ef{ef}_pmc.json"]))
     res = {
         "workload": f"y = x plus.times A (GrB_vxm, dense fp64 x) on R-MAT s{sc} ef {ef} fp64 U[0,1) "
                     f"(com-Orkut stand-in)",
@@ -514,7 +515,7 @@ def config4_masked_spgemm(lib, torch, stream, O, args, s4, cpu=False):
     by4 = 2 * (12 * nnz4 + 8 * (n4 + 1)) + 4 * nnz4 + 8 * (n4 + 1) + 12 * nnzc + 8 * (n4 + 1)
     for h in (B, C):
         lib.GrB_Matrix_free(ctypes.byref(h))
-    traffic, src = _profile_traffic(f"r04_config4_s{s4}_pmc.json", f"r03_config4_s{s4}_pmc.json")
+    traffic, src = _profile_traffic(f"r05_config4_s{s4}_pmc.json", f"r04_config4_s{s4}_pmc.json")
     res = {
         "workload": f"C<A.S> = A min.plus A (GrB_mxm, GrB_DESC_S), R-MAT s{s4}, INT64 weights in [1,255]",
         "nnz_A": nnz4, "nnz_C": nnzc, "ms": t4 * 1e3, "gteps": work / t4 / 1e9,
@@ -767,7 +768,8 @@ def config5_spgemm(lib, torch, stream, O, dist, world, rank, args, sc, cpu=False
         tot = [int(x) for x in tt.tolist()]
     prods_all, nnzc_all, nnza_all, nfail, by_all, st_all, rx_all = tot
     ok(lib.GrB_Matrix_free(ctypes.byref(A)), "free A")
-    traffic, src = _profile_traffic(f"r04_config5_s{sc}_pmc.json") if world == 1 else (None, None)
+    traffic, src = _profile_traffic(f"r05_config5_s{sc}_pmc.json", f"r04_config5_s{sc}_pmc.json") \
+        if world == 1 else (None, None)
     roof = _roofline(by_all / world, el, traffic, src, "one GrB_mxm call per GPU (k_row_flops, hash bins, "
                                                        "k_row_window, k_window_num, segmented sort)")
     roof["alg_bytes_def"] = ("SURVEY 8(d) config 5, per GPU: 12 nnz(A_r) + 12 nnz(B) + 12 nnz(C_r) + row pointers "
@@ -1228,10 +1230,11 @@ def main():
                        "parallelism": f"1-D row shards x{world}" if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": (achieved / PEAK_HBM_GBS) if achieved else None, "traffic": traffic,
+                         "traffic_source": os.path.relpath(args.traffic_file, ROOT) if traffic else None,
                          "kernel": "k_iso_work (+ k_dir_prep on a BFS's first level)",
                          "rocprof_note": "timed with the level speculation off (one launch per level); under "
                                          "rocprofv3 the speculating loop shows one more, empty k_iso_work per BFS "
-                                         "(the level after the last) -- profiles/r04_bfs_nospec_kernel_stats.csv "
+                                         "(the level after the last) -- profiles/r05_bfs_nospec_kernel_stats.csv "
                                          "is the BFS with bfs_spec=1, whose average is this one's",
                          "avg_launch_us": kern_ms * 1e3 / launches,
                          "launches": launches, "alg_bytes_per_launch": alg_bytes / launches,
