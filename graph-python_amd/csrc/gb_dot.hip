@@ -606,6 +606,12 @@ constexpr int DT_FLOG = 17;      // filter bits (log2)
 
 __device__ __forceinline__ uint32_t dt_hash(int32_t k) { return ((uint32_t)k * 0x9E3779B1u) >> (32 - DT_FLOG); }
 
+// LDS slot of X key i: a binary search over a power-of-two span probes keys m * 2^j - 1, which
+// all sit in one of the 64 banks while 2^j >= 64 (up to 64-way conflicts in the first seven
+// steps); skewing by i / 64 and i / 4096 spreads every step's probes over distinct banks
+constexpr int DT_KSLOTS = DT_CAP + DT_CAP / 64 + DT_CAP / 4096 + 1;
+__device__ __forceinline__ int dt_kp(int i) { return i + (i >> 6) + (i >> 12); }
+
 // fold z into T's 4- or 8-byte output slot (pieces of one entry meet here; exact monoids)
 template <class SR, class Z>
 __device__ __forceinline__ void dt_global_fold(const SR &sr, bool any_store, Z *slot, Z z) {
@@ -663,7 +669,7 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
     const int64_t *__restrict__ eYS, const int32_t *__restrict__ eO, const int32_t *__restrict__ eB,
     const int64_t *__restrict__ eQ, Z *__restrict__ tval, uint8_t *__restrict__ tflag, int dbg,
     const uint16_t *__restrict__ ePc, int pcap, unsigned long long *__restrict__ tctr, int chunk) {
-    __shared__ int32_t keys[DT_CAP];
+    __shared__ int32_t keys[DT_KSLOTS];  // X's keys at dt_kp(i)
     __shared__ uint32_t filt[1 << (DT_FLOG - 5)];
     __shared__ uint64_t estart[DT_SMAX / 64 + 1];     // bit f: an entry starts at flat element f
     __shared__ int32_t stage[DT_TB / 64][64 * DT_U];  // staged flat element | entry << 17
@@ -743,7 +749,7 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
             for (int j = 0; j < XPT; j++) {
                 if (tid + j * DT_TB < a) {
                     const int32_t k = xk[j];
-                    keys[tid + j * DT_TB] = k;
+                    keys[dt_kp(tid + j * DT_TB)] = k;
                     const uint32_t h = dt_hash(k);
                     atomicOr(&filt[h >> 5], 1u << (h & 31));
                 }
@@ -819,9 +825,9 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
                 int l = 0;  // number of X keys < kk
                 for (int st = ksteps - 1; st >= 0; st--) {
                     const int c = l + (1 << st);
-                    if (c <= a && keys[c - 1] < kk) l = c;
+                    if (c <= a && keys[dt_kp(c - 1)] < kk) l = c;
                 }
-                if (act && !(dbg & 1) && l < a && keys[l] == kk) {
+                if (act && !(dbg & 1) && l < a && keys[dt_kp(l)] == kk) {
                     X xv = X(), yv = X();
                     if (rv) {
                         xv = xvx[xs + l];
