@@ -14,6 +14,9 @@ import graphblas_amd as gb  # noqa: E402
 
 scale = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+for kv in sys.argv[3:]:  # library knobs k=v
+    k_, v_ = kv.split("=")
+    gb.set_knob(k_, int(v_))
 lib = gb.lib
 stream = torch.cuda.Stream()
 gb.set_stream(stream)
