@@ -53,17 +53,122 @@ static void scan_chunked(It in, int64_t *out, int64_t n) {
     gb_free(t);
 }
 
-void gb_exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n) {
-    // out has n+1 slots: out[0] = 0, out[i+1] = in[0] + ... + in[i]; any n (chunked)
-    scan_chunked(in, out, n);
-}
 
 struct gb_i32_plus {
     int64_t add;
     __host__ __device__ int64_t operator()(int32_t x) const { return (int64_t)x + add; }
 };
 
+// wave-tile scan of 4- or 8-byte integers (each + add_each), as the byte-flag scan below:
+// four consecutive items per lane per round, SCW_ROUNDS rounds per wave tile
+constexpr int SCW_ROUNDS = 8;
+constexpr int64_t SCW_TILE = 64 * 4 * SCW_ROUNDS;
+
+template <class T>
+__device__ __forceinline__ void scw_load4(const T *__restrict__ in, int64_t i, int64_t n, int64_t add, int64_t (&v)[4]) {
+    if (i + 4 <= n) {
+        if constexpr (sizeof(T) == 4) {
+            const int4 q = *reinterpret_cast<const int4 *>(in + i);
+            v[0] = (int64_t)q.x + add;
+            v[1] = (int64_t)q.y + add;
+            v[2] = (int64_t)q.z + add;
+            v[3] = (int64_t)q.w + add;
+        } else {
+            const longlong2 a = reinterpret_cast<const longlong2 *>(in + i)[0];
+            const longlong2 b = reinterpret_cast<const longlong2 *>(in + i)[1];
+            v[0] = a.x + add;
+            v[1] = a.y + add;
+            v[2] = b.x + add;
+            v[3] = b.y + add;
+        }
+    } else {
+        for (int b = 0; b < 4; b++) v[b] = i + b < n ? (int64_t)in[i + b] + add : 0;
+    }
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void k_scanw_sums(const T *__restrict__ in, int64_t add, int64_t n, int64_t ntiles,
+                                                    int64_t *__restrict__ tsum) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t t = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; t < ntiles; t += nw) {
+        const int64_t base = t * SCW_TILE;
+        int64_t s = 0;
+#pragma unroll
+        for (int r = 0; r < SCW_ROUNDS; r++) {
+            const int64_t i = base + (int64_t)r * 256 + 4 * lane;
+            int64_t v[4];
+            scw_load4(in, i, n, add, v);
+            s += v[0] + v[1] + v[2] + v[3];
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+        if (lane == 0) tsum[t] = s;
+    }
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void k_scanw_tiles(const T *__restrict__ in, int64_t add, int64_t n, int64_t ntiles,
+                                                     const int64_t *__restrict__ toff, int64_t *__restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t t = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; t < ntiles; t += nw) {
+        const int64_t base = t * SCW_TILE;
+        int64_t run = toff[t];
+#pragma unroll
+        for (int r = 0; r < SCW_ROUNDS; r++) {
+            const int64_t i = base + (int64_t)r * 256 + 4 * lane;
+            int64_t v[4];
+            scw_load4(in, i, n, add, v);
+            const int64_t sm = v[0] + v[1] + v[2] + v[3];
+            int64_t inc = sm;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int64_t y = __shfl_up(inc, off, 64);
+                if (lane >= off) inc += y;
+            }
+            const int64_t e = run + (inc - sm);
+            if (i + 4 <= n) {
+                longlong2 *o = reinterpret_cast<longlong2 *>(out + i);
+                o[0] = make_longlong2(e, e + v[0]);
+                o[1] = make_longlong2(e + v[0] + v[1], e + v[0] + v[1] + v[2]);
+            } else {
+                const int64_t v4[4] = {e, e + v[0], e + v[0] + v[1], e + v[0] + v[1] + v[2]};
+                for (int b = 0; b < 4; b++)
+                    if (i + b < n) out[i + b] = v4[b];
+            }
+            run += __shfl(inc, 63, 64);
+        }
+        if (t == ntiles - 1 && lane == 0) out[n] = run;
+    }
+}
+
+// the wave-tile path for n items from SCW_TILE * 64 up, with 16-byte aligned input and output
+template <class T>
+static bool scanw(const T *in, int64_t add, int64_t *out, int64_t n) {
+    if (n < SCW_TILE * 64 || ((uintptr_t)in & 15) || ((uintptr_t)out & 15) || gb_knob("scan_u8") == 1) return false;
+    const int64_t nt = (n + SCW_TILE - 1) / SCW_TILE;
+    int64_t *ts = gb_malloc_n<int64_t>(nt);
+    int64_t *to = gb_malloc_n<int64_t>(nt + 1);
+    const unsigned g = (unsigned)std::min<int64_t>((nt + 3) / 4, 8192);
+    hipLaunchKernelGGL(k_scanw_sums<T>, dim3(g), dim3(256), 0, gb_stream(), in, add, n, nt, ts);
+    GB_LAUNCH_CHECK();
+    scan_chunked(ts, to, nt);
+    hipLaunchKernelGGL(k_scanw_tiles<T>, dim3(g), dim3(256), 0, gb_stream(), in, add, n, nt, to, out);
+    GB_LAUNCH_CHECK();
+    gb_free(ts);
+    gb_free(to);
+    return true;
+}
+
+void gb_exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n) {
+    // out has n+1 slots: out[0] = 0, out[i+1] = in[0] + ... + in[i]; any n (chunked)
+    if (scanw(in, (int64_t)0, out, n)) return;
+    scan_chunked(in, out, n);
+}
+
 void gb_exclusive_scan_i32(const int32_t *in, int64_t add_each, int64_t *out, int64_t n) {
+    if (scanw(in, add_each, out, n)) return;
     scan_chunked(hipcub::TransformInputIterator<int64_t, gb_i32_plus, const int32_t *>(in, gb_i32_plus{add_each}), out,
                  n);
 }
