@@ -257,54 +257,56 @@ __global__ void k_dt_piece_count(dt_side s, int64_t nh, int cap, const int32_t *
 }
 
 // per pair: the entry's run of Y keys inside the piece's key range, cut into sub-entries of at
-// most cap keys (the task kernel's flat-space bound).  All of an entry's searches run in
-// lockstep -- the branchless lower bound's length sequence depends only on the Y list's length,
-// so up to 2 * DT_PB searches of a batch of pieces advance together with their loads in flight
-// (round 4 ran them one after another: 2 * pieces * log2(|Y|) dependent loads per entry)
-constexpr int DT_PB = 4;
+// most cap keys (the task kernel's flat-space bound).  Piece j's range is [X[j cap], X[(j+1) cap])
+// (the last: to the end): the Y keys between a piece's last key and the next piece's first are
+// in no piece of X, so they match nothing wherever they go, and one lower bound per piece start
+// sizes every piece (round 4 searched both ends of each piece: 2 np searches per entry, now
+// np + 1 per batch).  All of an entry's searches run in lockstep -- the branchless lower bound's
+// length sequence depends only on the Y list's length -- so a batch of DT_PB pieces advances its
+// DT_PB + 1 searches together with their loads in flight.
+constexpr int DT_PB = 8;
 
 __global__ void k_dt_piece_flags(dt_side s, int64_t nh, int cap, const int32_t *__restrict__ hG,
                                  const int64_t *__restrict__ hYS, const int32_t *__restrict__ hB,
                                  const int64_t *__restrict__ P, const int64_t *__restrict__ hpos,
                                  int32_t *__restrict__ cnt, int64_t *__restrict__ pys, int32_t *__restrict__ pb) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nh; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t g = hG[i], xs = s.xrp[g], a = s.xrp[g + 1] - xs;
+        const int64_t g = hG[i], xs = s.xrp[g];
         int64_t h0, h1;
         dt_group_span(s, hpos, g, h0, h1);
         const int64_t base = P[h0] + (i - h0), m = h1 - h0, np = P[i + 1] - P[i];
         const int64_t ys = hYS[i], ye = ys + hB[i];
         for (int64_t j0 = 0; j0 < np; j0 += DT_PB) {
-            int32_t key[2 * DT_PB];
-            int64_t bp[2 * DT_PB];
+            int32_t key[DT_PB + 1];
+            int64_t bp[DT_PB + 1];
+            bool end[DT_PB + 1];
 #pragma unroll
-            for (int u = 0; u < DT_PB; u++) {
-                const int64_t j = j0 + u < np ? j0 + u : np - 1;
-                const int64_t x0 = j * cap, x1 = (x0 + cap < a ? x0 + cap : a) - 1;
-                key[2 * u] = s.xci[xs + x0];
-                const int32_t k1 = s.xci[xs + x1];
-                key[2 * u + 1] = k1 == INT32_MAX ? INT32_MAX : k1 + 1;  // INT32_MAX: search to the end
-                bp[2 * u] = bp[2 * u + 1] = ys;
+            for (int u = 0; u <= DT_PB; u++) {
+                const int64_t j = j0 + u < np ? j0 + u : np;  // j == np: the end of the list
+                end[u] = j == np;
+                key[u] = end[u] ? INT32_MAX : s.xci[xs + j * cap];
+                bp[u] = ys;
             }
             int64_t n = ye - ys;
             while (n > 1) {
                 const int64_t half = n >> 1;
 #pragma unroll
-                for (int q = 0; q < 2 * DT_PB; q++)
+                for (int q = 0; q <= DT_PB; q++)
                     if (s.yci[bp[q] + half - 1] < key[q]) bp[q] += half;
                 n -= half;
             }
-            int64_t lb[2 * DT_PB];
+            int64_t lb[DT_PB + 1];
 #pragma unroll
-            for (int q = 0; q < 2 * DT_PB; q++) {
+            for (int q = 0; q <= DT_PB; q++) {
                 // bp is the last candidate: the lower bound is bp or bp + 1
                 lb[q] = (n == 1 && s.yci[bp[q]] < key[q]) ? bp[q] + 1 : bp[q];
-                if ((q & 1) && key[q] == INT32_MAX) lb[q] = ye;
+                if (end[q]) lb[q] = ye;
             }
 #pragma unroll
             for (int u = 0; u < DT_PB; u++) {
                 const int64_t j = j0 + u;
                 if (j >= np) break;
-                const int64_t lo = lb[2 * u], hi = lb[2 * u + 1] > lo ? lb[2 * u + 1] : lo;
+                const int64_t lo = lb[u], hi = lb[u + 1] > lo ? lb[u + 1] : lo;
                 const int64_t q = base + j * m;
                 pys[q] = lo;
                 pb[q] = (int32_t)(hi - lo);
