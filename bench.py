@@ -470,10 +470,22 @@ def config4_masked_spgemm(lib, torch, stream, O, args, s4, cpu=False):
     ok(lib.GxB_Matrix_prepare_transpose(B), "transpose")
     ok(lib.GrB_Matrix_nvals(ctypes.byref(nv), B), "nvals")
     nnz4 = nv.value
-    C = ctypes.c_void_p()
-    ok(lib.GrB_Matrix_new(ctypes.byref(C), lib.GrB_INT64, n4, n4), "C")
     sr4 = lib.GrB_MIN_PLUS_SEMIRING_INT64
-    t4 = _time_calls(torch, stream, lambda: ok(lib.GrB_mxm(C, B, None, sr4, B, B, lib.GrB_DESC_S), "mxm"), 3)
+    # each call writes a NEW C, as the reference's `semiring.min_plus(A @ A).new(mask=A.S)` does
+    # (SURVEY 3.4); the previous call's C is freed.  Round 4 re-used one C, so each timed call was
+    # the update C<M> = T over the previous result, which also merges C's existing entries.
+    cbox = [None]
+
+    def call4():
+        cn = ctypes.c_void_p()
+        ok(lib.GrB_Matrix_new(ctypes.byref(cn), lib.GrB_INT64, n4, n4), "C")
+        ok(lib.GrB_mxm(cn, B, None, sr4, B, B, lib.GrB_DESC_S), "mxm")
+        if cbox[0] is not None:
+            lib.GrB_Matrix_free(ctypes.byref(cbox[0]))
+        cbox[0] = cn
+
+    t4 = _time_calls(torch, stream, call4, 3)
+    C = cbox[0]
     bp = np.empty(n4 + 1, np.uint64)
     bi = np.empty(nnz4, np.uint64)
     bx = np.empty(nnz4, np.int64)
