@@ -68,4 +68,4 @@ for g in sys.argv[3:] or ["0"]:
         ts.append(time.perf_counter() - t0)
     t = min(ts)
     print(f"s{scale} {g}: nnz(A) {nnz} nnz(C) {nc} work {work:.3e} time {t*1e3:.2f} ms "
-          f"GTEPS {work / t / 1e9:.2f}", flush=True)
+          f"GTEPS {work / t / 1e9:.2f}  (all: {' '.join(f'{x * 1e3:.2f}' for x in ts)})", flush=True)
