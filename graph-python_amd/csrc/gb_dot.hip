@@ -506,10 +506,9 @@ __global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, dt_side s, dt_val
         int32_t xk[KPL];
 #pragma unroll
         for (int j = 0; j < KPL; j++) xk[j] = lane * KPL + j < a ? s.xci[xs + lane * KPL + j] : 0x7fffffff;
-        // X's values held beside the keys (read by a shuffle on a hit, no dependent load)
-        X xv[KPL];
-#pragma unroll
-        for (int j = 0; j < KPL; j++) xv[j] = (rv && lane * KPL + j < a) ? xvx[xs + lane * KPL + j] : X();
+        // X's values: read on a hit from the row just loaded (an L2 hit); round 4 held them in
+        // registers beside the keys and shuffled KPL of them (two 32-bit shuffles each for 8-byte
+        // values) for every 64 Y keys -- the kernel is bound by its shuffles, not by these loads
         for (int64_t pb = p0; pb < p1; pb += 64) {
             const int nb = __builtin_amdgcn_readfirstlane((int)std::min<int64_t>(64, p1 - pb));
             int32_t o_l = 0;
@@ -540,7 +539,6 @@ __global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, dt_side s, dt_val
                                 if (__shfl(xk[0], lo + st - 1, 64) < yk) lo += st;
                             // every lane takes part in the shuffle (a lane outside |Y| still serves its key)
                             const int32_t xl = __shfl(xk[0], lo, 64);
-                            xm = gb_shfl(xv[0], lo);
                             if (act && xl == yk) pos = lo;
                         } else {
                             int L = 0;  // last lane whose first key <= yk
@@ -553,16 +551,15 @@ __global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, dt_side s, dt_val
 #pragma unroll
                             for (int j = 0; j < KPL; j++) {
                                 const int32_t v = __shfl(xk[j], L, 64);
-                                const X vx = gb_shfl(xv[j], L);
-                                if (act && v == yk) {
-                                    pos = L * KPL + j;
-                                    xm = vx;
-                                }
+                                if (act && v == yk) pos = L * KPL + j;
                             }
                         }
                         if (pos >= 0) {
                             X yv = X();
-                            if (rv) yv = yvx[ys + f0 + lane];
+                            if (rv) {
+                                xm = xvx[xs + pos];
+                                yv = yvx[ys + f0 + lane];
+                            }
                             const Z z = dt_mult<SR, X, Z, SWAP>(sr, xm, yv, g, yk, o);
                             acc = found ? sr.add(acc, z) : z;
                             found = true;
