@@ -886,16 +886,26 @@ __global__ __launch_bounds__(HG, 8) void k_window_num(
     const int W = 1 << logW;
     const int NWD = W >> 5;
     uint32_t *bm = (uint32_t *)smem;
-    int32_t *prew = (int32_t *)(smem + (size_t)NWD * 4);
-    S *vals = (S *)(smem + (size_t)NWD * 8);
+    // exclusive popcount prefix per 64-bit word pair, 16 bits relative to its 2^16-column half
+    // (s_hb): W/32 bytes instead of round 4's 32-bit prefix per word (W/8), so 2^17-column
+    // windows still fit two workgroups per CU
+    uint16_t *pre16 = (uint16_t *)(smem + (size_t)NWD * 4);
+    S *vals = (S *)(smem + (size_t)NWD * 4 + (size_t)NWD);
     S *stz = vals + vcap;                                  // DET: staged values
     uint16_t *sto = (uint16_t *)(stz + (DET ? TILE : 0));  // DET: staged slot offsets in the owner's slice
     __shared__ win_sweep_lds L;
     __shared__ int32_t s_cnt[DET ? WP : 1][NW][NW];
     __shared__ int64_t s_wsum[NW];
     __shared__ int32_t s_wmin[NW];
+    __shared__ int32_t s_hb[8];  // window prefix at each 2^16-column half (W <= 2^19)
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const bool rv = SR::reads_values && avx && bvx;
+    // the window's exclusive prefix at word q (q even: a pair boundary); pre16 holds the prefix's
+    // low 16 bits, and inside one 2^16-column half it grows by less than 2^16 from s_hb
+    auto wpre = [&](int q) -> int32_t {
+        const int32_t hb = s_hb[q >> 11];
+        return hb + (int32_t)(((uint32_t)pre16[q >> 1] - (uint32_t)hb) & 0xffffu);
+    };
     Z idv = Z();
     const bool has_id = mon_identity<Z>(mon, idv);
     const S ids = to_slot<Z, S>(idv);
@@ -983,7 +993,8 @@ __global__ __launch_bounds__(HG, 8) void k_window_num(
             }
             // sorted columns of the window: each thread writes the set bits of its own words
             for (int q = q0; q < q1; q++) {
-                prew[q] = run;
+                if ((q & 2047) == 0) s_hb[q >> 11] = run;
+                if (!(q & 1)) pre16[q >> 1] = (uint16_t)run;
                 uint32_t bits = bm[q];
                 while (bits) {
                     cci[outpos + run++] = c0 + q * 32 + __builtin_ctz(bits);
@@ -1016,7 +1027,9 @@ __global__ __launch_bounds__(HG, 8) void k_window_num(
                             if (ok[u]) {
                                 z[u] = sr.mult(av[u], bv[u], i, L.k[sx[u]], c[u] + c0);
                                 const int q = c[u] >> 5;
-                                rk[u] = prew[q] + __popc(bm[q] & ((1u << (c[u] & 31)) - 1u)) - rbase;
+                                const int qe = q & ~1;
+                                rk[u] = wpre(qe) + ((q & 1) ? __popc(bm[qe]) : 0) +
+                                        __popc(bm[q] & ((1u << (c[u] & 31)) - 1u)) - rbase;
                             }
                         }
                         if constexpr (DET) {
@@ -1050,7 +1063,7 @@ __global__ __launch_bounds__(HG, 8) void k_window_num(
             // value groups of < vcap entries, each a run of 256-column chunks
             const int NB = W >> 8;
             const int64_t GV = vcap - 256;
-            auto chunk_pre = [&](int b) -> int64_t { return b < NB ? (int64_t)prew[b * 8] : m; };
+            auto chunk_pre = [&](int b) -> int64_t { return b < NB ? (int64_t)wpre(b * 8) : m; };
             auto first_chunk = [&](int64_t key) {  // first b in [0, NB) with chunk_pre(b) >= key, else NB
                 int lo = 0, hi = NB;
                 while (lo < hi) {
@@ -1352,15 +1365,21 @@ void spgemm_hash_run(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, const gb_
             // 8192 LDS values and 4 products per thread held one workgroup of 153 KB LDS per
             // CU at 4 waves per SIMD; config 5 s19 219 -> 204 ms at 2^16 / 3072 / 2, <= 64 VGPRs)
             int lw = SYM ? win_log(19) : (sizeof(Z) < 4 ? std::max(9, win_log(13)) : win_log(16));
-            // knob window_lw (numeric, 4-8-byte values): wider windows, fewer sweeps of a row's A
-            // entries per row (one workgroup per CU above 2^16 columns: the bitmap and its
-            // prefix take W/4 bytes of LDS)
+            // knob window_lw (numeric, 4-8-byte values): wider windows, fewer windows per row but
+            // more value groups per window (round 5: 2^17 slower at s19 and s20 even at two
+            // workgroups per CU)
             const int64_t klw = gb_knob("window_lw");
             if (!SYM && sizeof(Z) >= 4 && klw >= 10 && klw <= 18) lw = win_log((int)klw);
-            int vcap = (SYM || !VALS) ? 0 : (sizeof(Z) < 4 ? (1 << lw) : 3072);
-            // tests: a small LDS value capacity sends windows to the C-resident accumulation
+            // round 5: the window prefix takes W/32 bytes instead of W/8, and the LDS it frees
+            // holds more values per group (fewer value groups, hence fewer sweeps of the row's A
+            // entries): 4480 slots keep two workgroups per CU (tools/spgemm_time.py, one box:
+            // 3072 / 3584 / 4096 / 4480 -> s20 510 / 484 / 488 / 480 ms, s19 168.5 / - / 157.0 /
+            // 154.6 ms; 6144 / 8192 drop to one workgroup per CU: s20 668 / 650 ms)
+            int vcap = (SYM || !VALS) ? 0 : (sizeof(Z) < 4 ? (1 << lw) : 4480);
+            // tests: a small LDS value capacity sends windows to the C-resident accumulation (and
+            // A/B sweeps: up to 8192 for 4-8-byte values)
             const int64_t kv = gb_knob("window_vcap");
-            if (vcap && kv > 256 && kv < vcap) vcap = (int)kv;
+            if (vcap && kv > 256 && (kv < vcap || (sizeof(Z) >= 4 && kv <= 8192))) vcap = (int)kv;
             // grouped sweeps (one per vcap entries) up to this many, then C-resident accumulation
             const int64_t kg = gb_knob("window_in_c_groups");
             const int in_c_groups = kg > 0 ? (int)kg : 8;  // tools/sweep_in_c.sh: 2 226 ms, 4 208, 8 204, never 206 (config 5)
@@ -1389,7 +1408,7 @@ void spgemm_hash_run(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, const gb_
                 }
                 auto win = [&](auto detc) {
                     constexpr bool D = decltype(detc)::value;
-                    const size_t sh = (size_t)(1 << lw) / 4 + (size_t)vcap * sizeof(S) +
+                    const size_t sh = (size_t)(1 << lw) / 8 + (size_t)(1 << lw) / 32 + (size_t)vcap * sizeof(S) +
                                       (D ? (size_t)HG * WP * (sizeof(S) + 2) : 0);
                     set_lds(k_window_num<D, SRT, X, Z>, sh);
                     hipLaunchKernelGGL((k_window_num<D, SRT, X, Z>), dim3(hgrid(b.c[4], 1, 2048)), dim3(HG), sh,

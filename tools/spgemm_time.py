@@ -91,4 +91,4 @@ for rnd in range(reps):
 for s in settings:
     t = np.array(res[s])
     print(f"[{s or 'defaults'}] s{scale} nnzC {nv.value} ms median {np.median(t):.1f} min {t.min():.1f} "
-          f"| distinct digests over 3 runs: {len(dig[s])}", flush=True)
+          f"| distinct digests over 3 runs: {len(dig[s])} {sorted(dig[s])}", flush=True)
