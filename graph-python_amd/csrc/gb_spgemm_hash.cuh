@@ -1382,7 +1382,10 @@ void spgemm_hash_run(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, const gb_
             if (vcap && kv > 256 && (kv < vcap || (sizeof(Z) >= 4 && kv <= 8192))) vcap = (int)kv;
             // grouped sweeps (one per vcap entries) up to this many, then C-resident accumulation
             const int64_t kg = gb_knob("window_in_c_groups");
-            const int in_c_groups = kg > 0 ? (int)kg : 8;  // tools/sweep_in_c.sh: 2 226 ms, 4 208, 8 204, never 206 (config 5)
+            // round 3 (3072-value groups, s19): 2 226 ms, 4 208, 8 204, never 206; round 5 (4480-value
+            // groups, tools/spgemm_time.py): 4 / 5 / 6 / 7 / 8 -> s20 513 / 480 / 465 / 470 / 477 ms,
+            // s19 - / 157.1 / 153.4 / 153.0 / 154.1 ms
+            const int in_c_groups = kg > 0 ? (int)kg : 6;
             if constexpr (!SYM && VALS) {
                 // the long B rows' window index (knob window_index = 1: none; at most 1024 windows)
                 win_index wx;
