@@ -349,12 +349,21 @@ __device__ __forceinline__ long long gb_push_phase(int64_t nwords_u, const uint6
                                                   unsigned long long *__restrict__ tbits, gb_wlist &L,
                                                   const int64_t *__restrict__ hprow, long long &mfn,
                                                   const uint64_t *__restrict__ qbits, const gb_asg_dev &g,
-                                                  long long &adelta, bool serial = false) {
+                                                  long long &adelta, bool serial = false, bool prefetch = true) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const unsigned long long lt = (1ULL << lane) - 1;
     long long added = 0;
+    // the frontier words of this wave's first 16 steps, loaded before the hub chunks (round 5):
+    // lane l holds step l / 4's word l % 4, so a small frontier's scan costs one load round trip
+    // (overlapped with the hub test's) instead of one per step -- with one wave of workgroups a
+    // wave takes nwords / (4 * waves) steps, 4 at s22
+    uint64_t pre = 0;
+    {
+        const int64_t wl = wave * 4 + (int64_t)(lane >> 2) * nwaves * 4 + (lane & 3);
+        if (wl < nwords_u) pre = ubits[wl];
+    }
     // hub chunks: lane l of wave w tests table entry w + l * nwaves (a hub's
     // consecutive chunks land on different waves); hits are expanded in turn
     for (int64_t base = wave; base < nhubs; base += nwaves * 16) {
@@ -386,10 +395,16 @@ __device__ __forceinline__ long long gb_push_phase(int64_t nwords_u, const uint6
             }
         }
     }
-    // frontier words, 4 per wave step (lanes 0-3 load them)
-    for (int64_t w0 = wave * 4; w0 < nwords_u; w0 += nwaves * 4) {
+    // frontier words, 4 per wave step (lanes 0-3 load them; the first 16 steps' came above)
+    int step = 0;
+    for (int64_t w0 = wave * 4; w0 < nwords_u; w0 += nwaves * 4, step++) {
         const int64_t wl = w0 + (lane & 3);
-        const uint64_t mine = wl < nwords_u ? ubits[wl] : 0;
+        uint64_t mine;
+        if (prefetch && step < 16) {
+            mine = __shfl(pre, (step << 2) | (lane & 3), 64);
+        } else {
+            mine = wl < nwords_u ? ubits[wl] : 0;
+        }
         if (!__ballot(mine != 0)) continue;
         if (qbits) adelta += gb_asg_words(g, w0, nwords_u, mine, lane);
         int64_t p0[4], d[4];
@@ -749,7 +764,8 @@ struct gb_iso_args {
     int p1_steps, cap0;
     int dbg;                        // diagnostics (knob iso_dbg): 1 no mailbox, 2 no hint sum, 4 no work, 8 empty,
                                     // 16 pull without its segment list, 32 pull steps without probes (wrong results),
-                                    // 64 no finish, 128 the round-4 dependent read order (exact; A/B)
+                                    // 64 no finish, 128 the round-4 dependent read order (exact; A/B),
+                                    // 512 push without the frontier-word prefetch (exact; A/B)
     bool packed;                    // one-round finish (iso_finish_packed): n < 2^27
     const uint64_t *rows_nonempty;  // pull rows with entries (nullptr: all)
     const int32_t *phead;           // pull head per row, 4 int32 (nullptr: none; gb_view_pullfirst)
@@ -1315,7 +1331,8 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
         ;
     else if (push)
         cnt = gb_push_phase(nwords_u, ubits, prow, pcol, hubs, nhubs, H, mbits, mcomp,
-                            (unsigned long long *)tbits, L, a.hprow, mfn, qbits, a.asg, adelta, (a.dbg & 128) != 0);
+                            (unsigned long long *)tbits, L, a.hprow, mfn, qbits, a.asg, adelta, (a.dbg & 128) != 0,
+                            (a.dbg & 512) == 0);
     else
         cnt = gb_pull_iso_phase(nrows, rowptr, colidx, ubits, mbits, mcomp, tbits, L, a.hprow, mfn, a.p1_steps,
                                 a.cap0, a.rows_nonempty, qbits, a.asg, adelta, a.dbg,

@@ -885,7 +885,7 @@ static bool same_desc(const gb_desc &a, const gb_desc &b) {
 // notebook loop's shape
 static void spec_after_level(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr, GB_Obj *A, GB_Obj *u,
                              const gb_desc &d, bool vxm, const gb_asg &asg, bool direct, bool published) {
-    if (gb_knob("bfs_spec") == 1 || (gb_knob("iso_dbg") & ~128) != 0) return;  // 128: an A/B order, exact
+    if (gb_knob("bfs_spec") == 1 || (gb_knob("iso_dbg") & ~(128 | 512)) != 0) return;  // 128, 512: A/B orders, exact
     if (!direct || !published || accum || w != u || !mask || !d.replace || !d.comp || !d.structure) return;
     if (w->kind == GB_KIND_MATRIX || mask->kind == GB_KIND_MATRIX || A->kind != GB_KIND_MATRIX || A->cw) return;
     if (!spec_int_type(mask->type->code) || asg.bits != mask->bits || asg.vals != mask->dense) return;
