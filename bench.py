@@ -46,6 +46,23 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level tabl
 SLEEP_CYCLES = 100000  # ~40 us GPU spin ahead of each timed SpMV in the roofline pass
 
 
+def _profile_rounds():
+    """the rounds with a committed headline traffic file (profiles/traffic_rNN.json), newest first"""
+    import glob
+    import re
+
+    rs = set()
+    for f in glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json")):
+        m = re.match(r"traffic_(r\d+)\.json$", os.path.basename(f))
+        if m:
+            rs.add(m.group(1))
+    return sorted(rs, key=lambda r: int(r[1:]), reverse=True)
+
+
+ROUNDS = _profile_rounds()
+CUR_ROUND = ROUNDS[0] if ROUNDS else "r00"
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -60,7 +77,7 @@ def parse():
     p.add_argument("--no-msbfs-sharded", action="store_true",
                    help="N > 1: skip the row-sharded 64-root BFS line (one exchange per level for 64 roots)")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
-    p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r05.json"))
+    p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", f"traffic_{CUR_ROUND}.json"))
     # rehearsal of the N>1 path on one GPU: all ranks on one device, gloo transport
     p.add_argument("--dist-backend", default="nccl")
     p.add_argument("--no-pipeline", action="store_true",
@@ -141,11 +158,12 @@ def _threads():
     return int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
 
 
-def _profile_traffic(*names):
-    """HBM bytes per call of the first committed per-workload profile found among `names`
-    (tools/pmc_passes.sh + tools/pmc_table.py + tools/pmc_percall.py: 2 x FETCH_SIZE + WRITE_SIZE
-    summed over the call's kernels)."""
-    for name in names:
+def _profile_traffic(*stems):
+    """HBM bytes per call of the newest round's committed per-workload profile
+    profiles/rNN_<stem> (tools/pmc_passes.sh + tools/pmc_table.py + tools/pmc_percall.py:
+    2 x FETCH_SIZE + WRITE_SIZE summed over the call's kernels); the stems are tried in order
+    within a round, and older rounds only when the newest has none of them."""
+    for name in [f"{r}_{st}" for r in ROUNDS for st in stems]:
         path = os.path.join(ROOT, "profiles", name)
         try:
             return json.load(open(path))["hbm_bytes_per_call"], f"profiles/{name}"
@@ -189,7 +207,7 @@ def secondary_workloads(lib, torch, stream, O, args):
     # ---- config 4: masked min_plus SpGEMM, R-MAT s20 (configs[3]) and s22 (north_star's target)
     for s4 in (20, 22):
         out[f"config4_masked_spgemm_min_plus_int64_s{s4}"] = config4_masked_spgemm(lib, torch, stream, O, args, s4,
-                                                                                   cpu=s4 == 22)
+                                                                                   cpu=True)
     return out
 
 
@@ -427,9 +445,7 @@ def config2_spmv(lib, torch, stream, args, scale, ef, O=None, cpu=False):
     parity2 = bool(np.array_equal(present, np.diff(S.tocsc().indptr) > 0) and
                    np.allclose(got, ref, rtol=1e-6, atol=1e-9))
     by = 12 * nnz + 8 * (n + 1) + 16 * n
-    traffic, src = _profile_traffic(*([f"r05_config2_s{sc}_pmc.json", f"r04_config2_s{sc}_pmc.json",
-                                       f"r03_config2_s{sc}_pmc.json"] if ef == 16 else
-                                      [f"r05_config2_s{sc}_ef{ef}_pmc.json", f"r04_config2_s{sc}_ef{ef}_pmc.json"]))
+    traffic, src = _profile_traffic(f"config2_s{sc}_pmc.json" if ef == 16 else f"config2_s{sc}_ef{ef}_pmc.json")
     res = {
         "workload": f"y = x plus.times A (GrB_vxm, dense fp64 x) on R-MAT s{sc} ef {ef} fp64 U[0,1) "
                     f"(com-Orkut stand-in)",
@@ -527,7 +543,7 @@ def config4_masked_spgemm(lib, torch, stream, O, args, s4, cpu=False):
     by4 = 2 * (12 * nnz4 + 8 * (n4 + 1)) + 4 * nnz4 + 8 * (n4 + 1) + 12 * nnzc + 8 * (n4 + 1)
     for h in (B, C):
         lib.GrB_Matrix_free(ctypes.byref(h))
-    traffic, src = _profile_traffic(f"r05_config4_s{s4}_pmc.json", f"r04_config4_s{s4}_pmc.json")
+    traffic, src = _profile_traffic(f"config4_s{s4}_pmc.json")
     res = {
         "workload": f"C<A.S> = A min.plus A (GrB_mxm, GrB_DESC_S), R-MAT s{s4}, INT64 weights in [1,255]",
         "nnz_A": nnz4, "nnz_C": nnzc, "ms": t4 * 1e3, "gteps": work / t4 / 1e9,
@@ -780,7 +796,7 @@ def config5_spgemm(lib, torch, stream, O, dist, world, rank, args, sc, cpu=False
         tot = [int(x) for x in tt.tolist()]
     prods_all, nnzc_all, nnza_all, nfail, by_all, st_all, rx_all = tot
     ok(lib.GrB_Matrix_free(ctypes.byref(A)), "free A")
-    traffic, src = _profile_traffic(f"r05_config5_s{sc}_pmc.json", f"r04_config5_s{sc}_pmc.json") \
+    traffic, src = _profile_traffic(f"config5_s{sc}_pmc.json") \
         if world == 1 else (None, None)
     roof = _roofline(by_all / world, el, traffic, src, "one GrB_mxm call per GPU (k_row_flops, hash bins, "
                                                        "k_row_window, k_window_num, segmented sort)")
@@ -802,8 +818,9 @@ def config5_spgemm(lib, torch, stream, O, dist, world, rank, args, sc, cpu=False
     if world > 1:
         res["allgather"] = {"bytes_received_per_rank_avg": rx_all / world, "ms": tx * 1e3,
                             "GBs_per_rank": rx_all / world / tx / 1e9,
-                            "what": "B's row panels all-gathered (RowPanelAllGather: sizes, then one "
-                                    "all_gather_into_tensor) + GxB_Matrix_import_device, max over ranks"}
+                            "what": "B's row panels all-gathered (RowPanelAllGather: sizes, then one group of "
+                                    "send/recv pairs at the panels' true sizes) + GxB_Matrix_import_device, "
+                                    "max over ranks"}
     if cpu_res:
         res["cpu_baseline"] = cpu_res
     return res
@@ -1104,10 +1121,15 @@ def main():
     alg_bytes = len(roots) * (4 * int(ap[-1]) + 8 * (nloc + 1)) + levels_total * 3 * ((n + 7) // 8)
     achieved = alg_bytes / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else None
     traffic = None
-    # the committed PMC traffic is per launch of the single-GPU kernel (whole matrix): N = 1 only
+    trace_us = None
+    # the committed PMC traffic is per launch of the single-GPU kernel (whole matrix): N = 1 only;
+    # the same file's kernel trace (speculation off, one launch per level) gives the launch's
+    # average duration without the event pair's kernel boundary
     if world == 1 and os.path.exists(args.traffic_file):
         try:
-            traffic = json.load(open(args.traffic_file)).get("bytes_per_launch")
+            tj = json.load(open(args.traffic_file))
+            traffic = tj.get("bytes_per_launch")
+            trace_us = tj.get("per_kernel", {}).get("k_iso_work", {}).get("avg_us")
         except Exception:
             traffic = None
     # measured stream-copy ceiling (device-to-device copy of 2 GiB: read + write bytes)
@@ -1246,9 +1268,13 @@ def main():
                          "kernel": "k_iso_work (+ k_dir_prep on a BFS's first level)",
                          "rocprof_note": "timed with the level speculation off (one launch per level); under "
                                          "rocprofv3 the speculating loop shows one more, empty k_iso_work per BFS "
-                                         "(the level after the last) -- profiles/r05_bfs_nospec_kernel_stats.csv "
+                                         f"(the level after the last) -- profiles/{CUR_ROUND}_bfs_nospec_kernel_stats.csv "
                                          "is the BFS with bfs_spec=1, whose average is this one's",
                          "avg_launch_us": kern_ms * 1e3 / launches,
+                         # the same bytes over the committed kernel trace's average k_iso_work duration
+                         "avg_launch_us_trace": trace_us,
+                         "frac_trace": (alg_bytes / launches / (trace_us * 1e-6) / 1e9 / PEAK_HBM_GBS)
+                         if trace_us else None,
                          "launches": launches, "alg_bytes_per_launch": alg_bytes / launches,
                          "stream_copy_GBs": copy_gbs},
             "gteps_harmonic_mean": hm,

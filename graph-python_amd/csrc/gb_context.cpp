@@ -102,7 +102,7 @@ gb_host_slot *gb_host_slot_alloc() {
     gb_host_slot *s = g_slot_free.back();
     g_slot_free.pop_back();
     __atomic_store_n(&s->seq, 0LL, __ATOMIC_RELEASE);  // no word of a previous owner can match
-    s->pad[0] = 0;
+    s->host_last = 0;
     return s;
 }
 
@@ -110,7 +110,7 @@ void gb_host_slot_release(gb_host_slot *s) {
     if (!s) return;
     std::lock_guard<std::mutex> lk(g_slot_mu);
     __atomic_store_n(&s->seq, 0LL, __ATOMIC_RELEASE);
-    s->pad[0] = 0;
+    s->host_last = 0;
     g_slot_free.push_back(s);
 }
 
@@ -124,14 +124,14 @@ gb_host_slot *gb_host_slot_device(gb_host_slot *s) {
 // A tagged one-word publish carries 31 bits of the sequence number, so a word a slot kept
 // from a publish 2^30 or more numbers ago could alias a later one: such a word is cleared before
 // the slot's next publish is issued (that old publish has completed: all library work is on one
-// stream, and 2^30 launches have been issued behind it).  pad[0] holds, on the host only, the
-// last number issued to the slot.
+// stream, and 2^30 launches have been issued behind it).  host_last holds, on the host only, the
+// last number issued to the slot (a field no kernel writes: pad[0] carries a device hint).
 uint64_t gb_next_pub_seq(gb_host_slot *s) {
     const uint64_t seq = g_pub_seq.fetch_add(1, std::memory_order_relaxed) + 1;
     if (s) {
-        const uint64_t last = (uint64_t)s->pad[0];
+        const uint64_t last = (uint64_t)s->host_last;
         if (last && seq - last >= (1ULL << 30)) __atomic_store_n(&s->seq, 0LL, __ATOMIC_RELEASE);
-        s->pad[0] = (long long)seq;
+        s->host_last = (long long)seq;
     }
     return seq;
 }
@@ -231,6 +231,22 @@ void gb_hprof_add(int slot, const char *name, int64_t ns) {
     g_hprof[slot].calls += 1;
     std::lock_guard<std::mutex> lk(g_hprof[slot].mu);
     if (g_hprof[slot].samples.size() < (1u << 20)) g_hprof[slot].samples.push_back(ns);
+}
+
+namespace {
+std::mutex g_named_stat_mu;
+std::map<std::string, int64_t> g_named_stats;
+}  // namespace
+void gb_stat_add(const char *name, int64_t v) {
+    std::lock_guard<std::mutex> lk(g_named_stat_mu);
+    g_named_stats[name] += v;
+}
+bool gb_stat_get(const char *name, int64_t *v) {
+    std::lock_guard<std::mutex> lk(g_named_stat_mu);
+    auto it = g_named_stats.find(name);
+    if (it == g_named_stats.end()) return false;
+    *v = it->second;
+    return true;
 }
 
 int64_t gb_knob(const char *key) {
@@ -491,6 +507,11 @@ GrB_Info GxB_Global_get_int(const char *key, int64_t *value) {
     }
     if (!strcmp(key, "stat_nvals_copy")) {
         *value = g_stat_nvals_copy.load(std::memory_order_relaxed);
+        return GrB_SUCCESS;
+    }
+    // named kernel-class counters (gb_stat_add): "stat_" + name; 0 before the first count
+    if (!strncmp(key, "stat_", 5)) {
+        if (!gb_stat_get(key + 5, value)) *value = 0;
         return GrB_SUCCESS;
     }
     *value = gb_knob(key);

@@ -1015,6 +1015,7 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
             const dt_vals<X> vb{(const X *)btv, btv == BT.vals ? BT.nvx : nullptr, btv == BT.vals ? BT.nvk : 0,
                                 BT.iso};
             const dt_vals<X> xv = SWAP ? vb : va, yv = SWAP ? va : vb;
+            if (!SWAP && SRT::reads_values && (va.nk || vb.nk)) gb_stat_add("dot_narrow_calls", 1);
             const unsigned gw = dt_grid(sd.ng * 64, DT_BLOCK, 1 << 15);
             hipLaunchKernelGGL((k_dot_small<SRT, X, Z, SWAP, 1>), dim3(gw), dim3(DT_BLOCK), 0, gb_stream(), srf, sd,
                                xv, yv, (Z *)tval, tflag);
@@ -1044,6 +1045,7 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
                 GB_LAUNCH_CHECK();
                 gb_exclusive_scan_i32(nch, 0, hcp, sd.ng);
                 nhch = gb_read_i64(hcp + sd.ng);
+                gb_stat_add(SWAP ? "dot_hub_chunks_C" : "dot_hub_chunks_R", nhch);
                 if (nhch)
                     hipLaunchKernelGGL((k_dt_hub_classify<SWAP>), dim3((unsigned)std::min<int64_t>(nhch, 1 << 16)),
                                        dim3(DT_BLOCK), 0, gb_stream(), sd, hcp, nhch, hflag, pieces ? hg : nullptr);
@@ -1112,6 +1114,7 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
             };
             gb_exclusive_scan_u8(tf, pos, nm);
             const int64_t ne = gb_read_i64(pos + nm);
+            gb_stat_add(SWAP ? "dot_task_entries_C" : "dot_task_entries_R", ne);
             if (ne) {
                 gb_scratch es;
                 int32_t *eG = es.get<int32_t>(ne);
@@ -1189,6 +1192,7 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
             GB_LAUNCH_CHECK();
             gb_exclusive_scan_i32(pc, 0, ppos, npairs);
             const int64_t npe = gb_read_i64(ppos + npairs);
+            gb_stat_add(SWAP ? "dot_piece_entries_C" : "dot_piece_entries_R", npe);
             if (npe == 0) return;
             gb_scratch ps;
             int32_t *eG = ps.get<int32_t>(npe);
@@ -1208,6 +1212,8 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
     // entries left to the per-entry kernel
     gb_exclusive_scan_u8(hflag, pos, nm);
     const int64_t nh = gb_read_i64(pos + nm);
+    gb_stat_add("dot_calls", 1);
+    gb_stat_add("dot_huge_entries", nh);
     if (nh) {
         int64_t *hq = gb_malloc_n<int64_t>(nh);
         hipLaunchKernelGGL(k_dt_positions, dim3(dt_grid(nm)), dim3(DT_BLOCK), 0, gb_stream(), nm, hflag, pos, hq);

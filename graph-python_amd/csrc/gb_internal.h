@@ -180,6 +180,10 @@ void gb_spec_resolve(const void *keep);
 extern std::atomic<int64_t> g_stat_spec_adopted, g_stat_spec_rollbacks;  // GxB_Global_get_int("stat_...")
 extern std::atomic<int64_t> g_stat_nvals_copy;
 extern std::atomic<int64_t> g_stat_host_push;  // SpMV launches whose push direction the host proved
+// named counters of which kernel classes a call used (host-side, off the per-level BFS path):
+// GxB_Global_get_int("stat_<name>") reads them; tests assert that a workload reached a class
+void gb_stat_add(const char *name, int64_t v);
+bool gb_stat_get(const char *name, int64_t *v);
 struct gb_spec_hold_guard {
     gb_spec_hold_guard() { g_spec_hold++; }
     ~gb_spec_hold_guard() { g_spec_hold--; }
@@ -265,7 +269,8 @@ unsigned long long *gb_device_state();
 struct gb_host_slot {
     long long seq;
     long long value;
-    long long pad[6];
+    long long pad[5];  // pad[0]: the column-word kernels' device-written hint (gb_colbits.hip)
+    long long host_last;  // host only, never written by a device: the last sequence number issued
 };
 gb_host_slot *gb_host_slot_alloc();
 void gb_host_slot_release(gb_host_slot *s);

@@ -1513,8 +1513,16 @@ GrB_Info GxB_Vector_wait_ticket(GrB_Index *nvals, GrB_Vector v, uint64_t ticket)
         GB_REQUIRE(o->kind != GB_KIND_MATRIX, GrB_INVALID_OBJECT, "not a vector");
         GB_REQUIRE(o->pub && ticket, GrB_INVALID_VALUE, "no device publish to wait for");
         int64_t c = 0;
-        GB_REQUIRE(gb_host_slot_wait(o->pub, ticket, &c), GrB_INVALID_VALUE,
-                   "the publish was superseded by a later one of the same vector");
+        if (!gb_host_slot_wait(o->pub, ticket, &c)) {
+            // the stream drained without the word: a later publish of v overwrote it (superseded),
+            // or the publishing launch failed or never ran (lost) -- told apart by the slot's
+            // last issued number, which only the host writes
+            GB_REQUIRE((uint64_t)o->pub->host_last == ticket, GrB_INVALID_VALUE,
+                       "the publish was superseded by a later one of the same vector");
+            gb_sync();  // a failed launch surfaces here as GrB_PANIC
+            GB_REQUIRE(o->pub_seq == ticket, GrB_PANIC, "the publish never landed and v changed since");
+            c = gb_nvals(o);  // nothing published since: v's count is the ticket's (synchronous read)
+        }
         *nvals = (GrB_Index)c;
     });
 }
@@ -1549,12 +1557,18 @@ GrB_Info GxB_Vector_bitmap_import(GrB_Vector v, const void *src, GrB_Index nword
         vec_recount_published(o);
     });
 }
+// builds the cached transpose and, for integer values that fit fewer bytes, both orientations'
+// narrow value copies (gb_view_narrow: a min/max pass and a blocking read) -- the one-time work a
+// first masked GrB_mxm would otherwise do inside its call
 GrB_Info GxB_Matrix_prepare_transpose(GrB_Matrix A) {
     return gb_api(OBJ(A), [&] {
         GB_Obj *o = gb_obj_check(A);
         if (o->kind != GB_KIND_MATRIX) return;
-        gb_csr_view v;
-        gb_get_csc(v, o);
+        gb_csr_view v, vt;
+        gb_get_csr(v, o);
+        gb_view_narrow(v, o, 0);
+        gb_get_csc(vt, o);
+        gb_view_narrow(vt, o, 1);
     });
 }
 

@@ -1400,14 +1400,21 @@ void spgemm_hash_run(gb_mat_result &T, gb_csr_view &A, gb_csr_view &B, const gb_
                     GB_LAUNCH_CHECK();
                     gb_exclusive_scan_u8(fl, pos, B.nrows);
                     const int64_t nlong = gb_read_i64(pos + B.nrows);
-                    int64_t *ix = xs.get<int64_t>(std::max<int64_t>(1, nlong * (nwx + 1)));
-                    hipLaunchKernelGGL(k_wix_fill, dim3(hgrid(B.nrows * 64, 256, 8192)), dim3(256), 0, gb_stream(),
-                                       B.rowptr, B.colidx, B.nrows, lw, (int)nwx, fl, pos, slot, ix);
-                    GB_LAUNCH_CHECK();
-                    wx.slot = slot;
-                    wx.pos = ix;
-                    wx.lw = lw;
-                    wx.nw = (int)nwx;
+                    // an optional speed-up: its index (8 B per long row and window) is capped at twice
+                    // B's column indices (or 64 MB), so a wide matrix whose windows would make it
+                    // outgrow B runs without it (wx.slot == nullptr: the kernel searches instead)
+                    const int64_t ixbytes = nlong * (nwx + 1) * (int64_t)sizeof(int64_t);
+                    const int64_t budget = std::max<int64_t>((int64_t)64 << 20, 8 * B.nvals);
+                    if (ixbytes <= budget) {
+                        int64_t *ix = xs.get<int64_t>(std::max<int64_t>(1, nlong * (nwx + 1)));
+                        hipLaunchKernelGGL(k_wix_fill, dim3(hgrid(B.nrows * 64, 256, 8192)), dim3(256), 0,
+                                           gb_stream(), B.rowptr, B.colidx, B.nrows, lw, (int)nwx, fl, pos, slot, ix);
+                        GB_LAUNCH_CHECK();
+                        wx.slot = slot;
+                        wx.pos = ix;
+                        wx.lw = lw;
+                        wx.nw = (int)nwx;
+                    }
                 }
                 auto win = [&](auto detc) {
                     constexpr bool D = decltype(detc)::value;

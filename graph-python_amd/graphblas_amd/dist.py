@@ -183,10 +183,14 @@ class RowPanelAllGather:
     follow rank order.  run() returns the whole B (rowptr int64[n+1], colidx, values,
     iso) on every rank.  RCCL has no gatherv: the panel sizes, iso flags and iso values
     are all-gathered first (four int64 per rank); then every rank packs its panel (row
-    pointers, column indices, values: 8-byte aligned parts of one byte buffer, padded to
-    the largest panel) and ONE all-gather moves all panels at once -- on the xGMI mesh a
-    single collective keeps every link busy, where one broadcast per owner and array
-    serialises 3 x world collectives.  The panels are unpacked into the assembled buffers
+    pointers, column indices, values: 8-byte aligned parts of one byte buffer) and the
+    panels move as ONE group of point-to-point pairs (`batch_isend_irecv`: rank k sends its
+    packed panel to every peer and receives each peer's at that panel's true size) -- an
+    all-gatherv over the xGMI mesh, one direct link per pair, all links busy at once.  Round 5
+    padded every panel to the largest one and used all_gather_into_tensor; with rows balanced
+    by products the panels' byte sizes differ widely and the padding was wasted link traffic
+    (VERDICT r05).  `last_rx_bytes` is the bytes this rank received in the last run().  The
+    panels are unpacked into the assembled buffers
     and the local row pointers shifted by the panel's entry offset.  The result is iso only
     when every panel is iso with the same value; otherwise iso panels are expanded into
     their part, so every rank issues the same collective sequence.  Issued on the library
@@ -194,6 +198,7 @@ class RowPanelAllGather:
 
     def __init__(self, dist, world, rank):
         self.dist, self.world, self.rank = dist, world, rank
+        self.last_rx_bytes = 0
 
     @staticmethod
     def _value_bits(values):
@@ -244,10 +249,9 @@ class RowPanelAllGather:
             if not all_iso:
                 out_vx.copy_(values[:1].expand(out_vx.numel()) if iso else values)
             return out_rp, out_ci, out_vx, all_iso
-        # pack this rank's panel (iso panels expanded when the result is not iso)
-        maxb = max(1, max(l[2] for l in lay))
-        o_ci, o_vx, _ = lay[r]
-        send = torch.zeros(maxb, dtype=torch.uint8, device=dev)
+        # pack this rank's panel (iso panels expanded when the result is not iso), at its true size
+        o_ci, o_vx, mine = lay[r]
+        send = torch.zeros(max(1, mine), dtype=torch.uint8, device=dev)
         nr, nnz = sz[r][0], sz[r][1]
         if nr:
             send[:nr * 8].view(torch.int64).copy_(rowptr[1:])
@@ -256,27 +260,40 @@ class RowPanelAllGather:
             if not all_iso:
                 vpart = send[o_vx:o_vx + nnz * vs].view(values.dtype)
                 vpart.copy_(values[:1].expand(nnz) if iso else values)
-        recv = torch.empty(W * maxb, dtype=torch.uint8, device=dev)
-        if self.dist.get_backend() == "nccl":
-            self.dist.all_gather_into_tensor(recv, send)
-        elif send.is_cuda:  # gloo rehearsal of the GPU path: stage through host memory
-            host = torch.empty(W * maxb, dtype=torch.uint8)
-            self.dist.all_gather(list(host.chunk(W)), send.cpu())
-            recv.copy_(host)
-        else:
-            self.dist.all_gather(list(recv.chunk(W)), send)
+        # every peer's panel at its own size: one group of send/recv pairs (RCCL groups them into
+        # one launch); the gloo rehearsal of the GPU path stages through host memory
+        stage = send.is_cuda and self.dist.get_backend() != "nccl"
+        src = send.cpu() if stage else send
+        recv = {k: torch.empty(lay[k][2], dtype=torch.uint8, device="cpu" if stage else dev)
+                for k in range(W) if k != r and lay[k][2]}
+        ops = []
         for k in range(W):
-            base = k * maxb
+            if k == r:
+                continue
+            if mine:
+                ops.append(self.dist.P2POp(self.dist.isend, src[:mine], k))
+            if k in recv:
+                ops.append(self.dist.P2POp(self.dist.irecv, recv[k], k))
+        if ops:
+            for q in self.dist.batch_isend_irecv(ops):
+                q.wait()
+        self.last_rx_bytes = sum(b.numel() for b in recv.values())
+        for k in range(W):
+            buf = send if k == r else recv.get(k)
             nr, nnz = sz[k][0], sz[k][1]
+            if buf is None:
+                continue
+            if stage and k != r:
+                buf = buf.to(dev)
             kc, kv, _ = lay[k]
             if nr:
-                out_rp[roff[k] + 1:roff[k + 1] + 1].copy_(recv[base:base + nr * 8].view(torch.int64))
+                out_rp[roff[k] + 1:roff[k + 1] + 1].copy_(buf[:nr * 8].view(torch.int64))
                 if eoff[k]:
                     out_rp[roff[k] + 1:roff[k + 1] + 1] += eoff[k]
             if nnz:
-                out_ci[eoff[k]:eoff[k + 1]].copy_(recv[base + kc:base + kc + nnz * 4].view(colidx.dtype))
+                out_ci[eoff[k]:eoff[k + 1]].copy_(buf[kc:kc + nnz * 4].view(colidx.dtype))
                 if not all_iso:
-                    out_vx[eoff[k]:eoff[k + 1]].copy_(recv[base + kv:base + kv + nnz * vs].view(values.dtype))
+                    out_vx[eoff[k]:eoff[k + 1]].copy_(buf[kv:kv + nnz * vs].view(values.dtype))
         return out_rp, out_ci, out_vx, all_iso
 
 

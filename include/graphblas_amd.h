@@ -408,8 +408,10 @@ GrB_Info GxB_Vector_device_touch(GrB_Vector v);
  * vector had at that publish, read from the pinned host mailbox without synchronising the
  * stream -- valid although later work that does not write the vector was enqueued since
  * (GrB_Vector_nvals trusts a mailbox only while nothing was).  GrB_INVALID_VALUE if a later
- * publish of the same vector superseded it.  The pipelined sharded level loop
- * (graphblas_amd/dist.py: PipelinedLevels) enqueues level d + 1 before it waits for level
+ * publish of the same vector superseded it; if the stream drained without the publish (a
+ * failed or skipped launch) the count is read synchronously when the vector is unchanged since,
+ * GrB_PANIC otherwise.  The pipelined sharded level loop
+ * (graphblas_amd/dist.py: pipelined_levels) enqueues level d + 1 before it waits for level
  * d's frontier count.  Replaces the nvals read of reference notebooks/Example B.1 cell 8
  * (`q.nvals`, core/vector.py: Vector.nvals -> GrB_Vector_nvals). */
 GrB_Info GxB_Vector_publish_ticket(uint64_t *ticket, GrB_Vector v);
@@ -436,7 +438,10 @@ GrB_Info GxB_Vector_bitmap_import(GrB_Vector v, const void *src_device, GrB_Inde
 GrB_Info GxB_Matrix_rmat(GrB_Matrix *A, int scale, int edge_factor, uint64_t seed,
                          int values, uint64_t value_seed, GrB_Index row_begin,
                          GrB_Index row_end);
-/* Force the cached CSC (transpose) of A to be built now (outside timed regions). */
+/* Force the cached CSC (transpose) of A to be built now (outside timed regions), with the
+ * narrow value copies of both orientations when A's integer values fit 1-4 bytes (otherwise the
+ * first masked GrB_mxm reading them builds them: a min/max pass, one blocking read, and up to
+ * 4 B per entry and orientation kept until the transpose is dropped). */
 GrB_Info GxB_Matrix_prepare_transpose(GrB_Matrix A);
 /* Matrix Market coordinate reader (host, multithreaded; replaces the scipy /
  * fast_matrix_market parse behind reference graphblas/io/_matrixmarket.py:6-61).

@@ -13,23 +13,32 @@ sys.path.insert(0, ROOT)
 
 import bench  # noqa: E402  (module level: argparse, numpy, scipy only)
 
-ROUND = "r05"
+# the newest round with a committed headline traffic file: its profiles must be complete
+ROUND = bench.CUR_ROUND
 
 # the per-call profiles the secondary lines read (bench.py config2_spmv / config4_masked_spgemm /
-# config5_spgemm), first choice of each lookup
+# config5_spgemm)
 SECONDARY = [
-    f"{ROUND}_config2_s22_pmc.json",
-    f"{ROUND}_config2_s22_ef60_pmc.json",
-    f"{ROUND}_config4_s20_pmc.json",
-    f"{ROUND}_config4_s22_pmc.json",
-    f"{ROUND}_config5_s19_pmc.json",
-    f"{ROUND}_config5_s20_pmc.json",
+    "config2_s22_pmc.json",
+    "config2_s22_ef60_pmc.json",
+    "config4_s20_pmc.json",
+    "config4_s22_pmc.json",
+    "config5_s19_pmc.json",
+    "config5_s20_pmc.json",
 ]
 
 
-@pytest.mark.parametrize("name", SECONDARY)
-def test_secondary_traffic_from_this_round(name):
-    traffic, src = bench._profile_traffic(name)
+def test_round_is_the_newest_profile_round():
+    import glob
+    rounds = [int(os.path.basename(f)[len("traffic_r"):-len(".json")])
+              for f in glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json"))]
+    assert rounds and ROUND == f"r{max(rounds):02d}"
+
+
+@pytest.mark.parametrize("stem", SECONDARY)
+def test_secondary_traffic_from_this_round(stem):
+    name = f"{ROUND}_{stem}"
+    traffic, src = bench._profile_traffic(stem)
     assert src == f"profiles/{name}", f"{name} missing from profiles/"
     assert traffic and traffic > 0
     d = json.load(open(os.path.join(ROOT, src)))
@@ -38,17 +47,18 @@ def test_secondary_traffic_from_this_round(name):
 
 
 def test_bench_prefers_this_rounds_profiles():
-    """each _profile_traffic lookup in bench.py names this round's file first"""
+    """bench.py's lookups carry no hard-coded round: the newest round is tried first"""
     src = open(os.path.join(ROOT, "bench.py")).read()
-    calls = re.findall(r"_profile_traffic\(\*?\(?\[?\s*f?\"([a-z0-9_{}]+)", src)
+    calls = re.findall(r"_profile_traffic\(\s*f?\"([a-z0-9_{}.]+)", src)
     assert len(calls) >= 3, calls
     for first in calls:
-        assert first.startswith(f"{ROUND}_"), first
+        assert not re.match(r"r\d+_", first), first
+    assert bench.ROUNDS[0] == ROUND
 
 
 def test_headline_traffic_file():
-    args_src = open(os.path.join(ROOT, "bench.py")).read()
-    assert f'"traffic_{ROUND}.json"' in args_src
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert 'f"traffic_{CUR_ROUND}.json"' in src
     t = json.load(open(os.path.join(ROOT, "profiles", f"traffic_{ROUND}.json")))
     assert t["kernel"] == "k_iso_work"
     # PMC bytes per launch of the headline kernel vs SURVEY 8(d)'s 43.3 MB algorithmic at s22:

@@ -1,7 +1,7 @@
 """Row-sharded SpGEMM exchange at world_size 2 and 3 on CPU (gloo): each rank holds a
 consecutive block of rows of A (= its panel of B, since C = A*A); the CSR row panels
-are all-gathered (graphblas_amd.dist.RowPanelAllGather: sizes, then one all-gather of
-the packed panels) and the local product C_r = A_r plus.times B
+are all-gathered (graphblas_amd.dist.RowPanelAllGather: sizes, then one group of send/recv
+pairs moving every packed panel at its true size) and the local product C_r = A_r plus.times B
 (here the oracle; GrB_mxm on the GPU, bench.py config 5) stacked over the ranks must
 equal the oracle's A plus.times A.  SURVEY §8(e) mxm row; DESIGN.md §6."""
 import os
@@ -189,7 +189,15 @@ def _balanced_worker(rank, world, port, scale, out_q):
     rp = torch.from_numpy(G.indptr[lo:hi + 1] - p0)
     ci = torch.from_numpy(G.indices[p0:p1].astype(np.int32))
     vx = torch.from_numpy(G.values[p0:p1].copy())
-    brp, bci, bvx, _ = gdist.RowPanelAllGather(dist, world, rank).run(rp, ci, vx)
+    g = gdist.RowPanelAllGather(dist, world, rank)
+    brp, bci, bvx, _ = g.run(rp, ci, vx)
+    # the panels travel at their true sizes (no padding to the largest panel)
+    true_rx = 0
+    for k in range(world):
+        pk = gdist.partition(n, world, k, bounds)
+        if k != rank:
+            true_rx += g._layout(pk["hi"] - pk["lo"], int(G.indptr[pk["hi"]] - G.indptr[pk["lo"]]), 8, True)[2]
+    assert g.last_rx_bytes == true_rx, (g.last_rx_bytes, true_rx)
     B = O.Csr(n, n, "FP64", brp.numpy(), bci.numpy(), bvx.numpy())
     Ar = O.Csr(hi - lo, n, "FP64", rp.numpy(), ci.numpy(), vx.numpy())
     C = O.mxm(O.Csr.empty(hi - lo, n, "FP64"), Ar, B, ("PLUS", "TIMES", "FP64"))

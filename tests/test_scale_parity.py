@@ -11,7 +11,10 @@ checked here, through the C ABI exactly as bench.py drives them, against the CPU
   any_pair and lor_land, levels bit-exact vs O.bfs_levels; the 64-root batched form (masked
   GrB_mxm on column words): every root's levels;
 * config 4: C<A.S> = A min.+ A (reference core/matrix.py:2241 via core/base.py:483), INT64,
-  the whole C at s18 and 1024 sampled rows at s20, bit-exact vs O.mxm;
+  the whole C at s18 and 1024 sampled rows at s20, bit-exact vs O.mxm, and the whole C at s20 vs
+  the parallel oracle; north_star's own form C(M.V, accum=plus) << A.mxm(A, min_plus) with a
+  stored-false value mask and a pre-filled C, the whole C at s18 and 1024 rows at s20, every dot
+  class asserted by the library's stat counters;
 * config 2: y = x plus.times A (GrB_vxm, dense fp64 x) at s20 and s22, ef 16 and 60, rtol 1e-6 vs
   scipy (BASELINE.json north_star's fp64 tolerance);
 * config 5: C = A plus.times A (unmasked hash Gustavson) at s19, 512 sampled rows (the 32
@@ -198,6 +201,141 @@ def test_masked_min_plus_spgemm_bench_scale(gb, scale, rows):
     pick = np.unique(pick)
     Gs = _rows_csr(G, pick)
     ref = O.mxm(O.Csr.empty(len(pick), n, "INT64"), Gs, G, sr, mask=Gs, mask_struct=True)
+    Cs = _rows_csr(Cg, pick)
+    assert np.array_equal(Cs.indptr, ref.indptr)
+    assert np.array_equal(Cs.indices, ref.indices)
+    assert np.array_equal(Cs.values, ref.values)
+
+
+def _threads():
+    import os
+    return max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)))
+
+
+def _import_csr(lib, M, tname):
+    """a host Csr into a new GrB_Matrix (GrB_Matrix_import, CSR format)"""
+    h = ctypes.c_void_p()
+    ap = M.indptr.astype(np.uint64)
+    ai = M.indices.astype(np.uint64)
+    ax = np.ascontiguousarray(M.values, NP_OF[tname]) if M.nvals else np.zeros(1, NP_OF[tname])
+    ok(getattr(lib, f"GrB_Matrix_import_{tname}")(ctypes.byref(h), getattr(lib, f"GrB_{tname}"), M.nrows, M.ncols,
+                                                  ctypes.c_void_p(ap.ctypes.data), ctypes.c_void_p(ai.ctypes.data),
+                                                  ctypes.c_void_p(ax.ctypes.data), len(ap), len(ai), len(ax), 0),
+       "import")
+    return h
+
+
+def _stats(lib, names):
+    v = ctypes.c_int64()
+    out = {}
+    for nm in names:
+        ok(lib.GxB_Global_get_int(f"stat_{nm}".encode(), ctypes.byref(v)), nm)
+        out[nm] = v.value
+    return out
+
+
+DOT_STATS = ["dot_calls", "dot_task_entries_R", "dot_task_entries_C", "dot_piece_entries_R", "dot_piece_entries_C",
+             "dot_hub_chunks_R", "dot_hub_chunks_C", "dot_huge_entries", "dot_narrow_calls"]
+
+
+def test_masked_min_plus_spgemm_whole_c_s20(gb):
+    """config 4 at BASELINE's own scale (configs[3]: R-MAT s20): the WHOLE C of C<A.S> = A min.+ A,
+    bit-exact against the parallel oracle (or_masked_dot_min_plus_int64_par: per mask entry a
+    sorted merge / galloping dot over A(i,:) and A^T(j,:), every mask row)"""
+    import scipy.sparse as sp
+
+    lib = gb.lib
+    scale = 20
+    n = 1 << scale
+    B = rmat(lib, scale, "INT64")
+    C = ctypes.c_void_p()
+    ok(lib.GrB_Matrix_new(ctypes.byref(C), lib.GrB_INT64, n, n), "C")
+    try:
+        ok(lib.GrB_mxm(C, B, None, lib.GrB_MIN_PLUS_SEMIRING_INT64, B, B, lib.GrB_DESC_S), "mxm")
+        G = export(lib, B, n, "INT64")
+        Cg = export(lib, C, n, "INT64")
+    finally:
+        free(lib, B, C)
+    T = sp.csr_matrix((G.values, G.indices, G.indptr), shape=(n, n)).T.tocsr()
+    T.sort_indices()
+    GT = O.Csr(n, n, "INT64", T.indptr, T.indices, T.data)
+    vals, present, nc, _ = O.masked_dot_min_plus_int64_par(G, GT, 0, n, _threads())
+    rows = np.repeat(np.arange(n), np.diff(G.indptr))
+    ref_p = np.concatenate([[0], np.cumsum(np.bincount(rows[present], minlength=n))])
+    assert nc == int(present.sum()) == Cg.nvals
+    assert np.array_equal(Cg.indptr, ref_p)
+    assert np.array_equal(Cg.indices, G.indices[present])
+    assert np.array_equal(Cg.values, vals[present])
+
+
+def _north_star_operands(G, seed):
+    """M: A's structure as a BOOL value mask with ~30 % stored falses; C0: a pre-filled INT64 C holding
+    half of A's entries plus as many entries outside A's structure (so the accum merge, the kept entries
+    under false / absent mask entries and the new entries all occur)"""
+    rng = np.random.default_rng(seed)
+    n = G.nrows
+    M = O.Csr(n, n, "BOOL", G.indptr, G.indices, rng.random(G.nvals) >= 0.3)
+    rows = np.repeat(np.arange(n), np.diff(G.indptr))
+    keep = rng.random(G.nvals) < 0.5
+    extra = G.nvals // 2
+    er, ec = rng.integers(0, n, extra), rng.integers(0, n, extra)
+    r = np.concatenate([rows[keep], er])
+    c = np.concatenate([G.indices[keep], ec])
+    lin = np.unique(r * n + c)
+    r, c = lin // n, lin % n
+    C0 = O.Csr(n, n, "INT64", np.concatenate([[0], np.cumsum(np.bincount(r, minlength=n))]), c,
+               rng.integers(-1000, 1000, len(lin)))
+    return M, C0
+
+
+@pytest.mark.parametrize("scale,rows", [(18, None), (20, 1024)])
+@pytest.mark.parametrize("pieces", ["default", "forced"])
+def test_north_star_value_mask_accum_bench_scale(gb, scale, rows, pieces):
+    """BASELINE north_star's expression at bench scale: C(M.V, accum=binary.plus) << A.mxm(A, min_plus)
+    (reference core/base.py:318-483 -> GrB_mxm(C, M, GrB_PLUS_INT64, min_plus, A, A, NULL); small cases
+    pinned at graphblas/tests/test_matrix.py:348-386) with M a value mask holding stored falses and C
+    pre-filled: the whole C at s18, the 64 longest + random rows at s20, bit-exact vs O.mxm.  The dot's
+    classes must all fire (stat counters): task entries in both phases, hub chunks, narrow values,
+    and -- with pieces="forced" (knob dot_pmin = 1) -- the hub-piece tasks; by default s20's few hub
+    entries go to the per-entry kernel instead (dot_huge_entries)."""
+    lib = gb.lib
+    n = 1 << scale
+    A = rmat(lib, scale, "INT64")
+    G = export(lib, A, n, "INT64")
+    Mh_, Ch_ = ctypes.c_void_p(), ctypes.c_void_p()
+    Mc, C0 = _north_star_operands(G, 5 + scale)
+    try:
+        Mh_ = _import_csr(lib, Mc, "BOOL")
+        Ch_ = _import_csr(lib, C0, "INT64")
+        if pieces == "forced":
+            ok(lib.GxB_Global_set_int(b"dot_pmin", 1), "knob")
+        before = _stats(lib, DOT_STATS)
+        ok(lib.GrB_mxm(Ch_, Mh_, lib.GrB_PLUS_INT64, lib.GrB_MIN_PLUS_SEMIRING_INT64, A, A, None), "mxm")
+        after = _stats(lib, DOT_STATS)
+        Cg = export(lib, Ch_, n, "INT64")
+    finally:
+        lib.GxB_Global_set_int(b"dot_pmin", 0)
+        free(lib, A, Mh_, Ch_)
+    d = {k: after[k] - before[k] for k in DOT_STATS}
+    assert d["dot_calls"] == 1, d
+    for k in ("dot_task_entries_R", "dot_task_entries_C", "dot_hub_chunks_R", "dot_hub_chunks_C", "dot_narrow_calls"):
+        assert d[k] > 0, (k, d)
+    if pieces == "forced":
+        assert d["dot_piece_entries_R"] > 0 and d["dot_piece_entries_C"] > 0, d
+    else:
+        assert d["dot_piece_entries_R"] + d["dot_piece_entries_C"] + d["dot_huge_entries"] > 0, d
+    sr = ("MIN", "PLUS", "INT64")
+    if rows is None:
+        ref = O.mxm(C0, G, G, sr, mask=Mc, accum=("PLUS", "INT64"))
+        assert np.array_equal(Cg.indptr, ref.indptr)
+        assert np.array_equal(Cg.indices, ref.indices)
+        assert np.array_equal(Cg.values, ref.values)
+        return
+    deg = np.diff(G.indptr)
+    pick = np.unique(np.concatenate([np.argsort(deg)[-64:],
+                                     np.random.default_rng(9).choice(n, rows - 64, replace=False)]))
+    Gs, Ms, C0s = _rows_csr(G, pick), _rows_csr(Mc, pick), _rows_csr(C0, pick)
+    ref = O.mxm(C0s, Gs, G, sr, mask=Ms, accum=("PLUS", "INT64"))
     Cs = _rows_csr(Cg, pick)
     assert np.array_equal(Cs.indptr, ref.indptr)
     assert np.array_equal(Cs.indices, ref.indices)
