@@ -82,6 +82,9 @@ def parse():
     p.add_argument("--dist-backend", default="nccl")
     p.add_argument("--no-pipeline", action="store_true",
                    help="N > 1: wait for each level's count before enqueuing the next (round-4 loop)")
+    p.add_argument("--exchange", default="peer", choices=["allgather", "peer"],
+                   help="N > 1 BFS frontier exchange: host-issued all-gather (RCCL / gloo), or device-initiated "
+                        "writes into IPC-mapped peer windows (GxB_PeerWindow_*, no collective per level)")
     p.add_argument("--partition", default="balanced", choices=["balanced", "equal"],
                    help="N > 1 BFS: vertex ranges balanced by the shards' entries, or equal word slots")
     p.add_argument("--device", type=int, default=None, help="override LOCAL_RANK's device")
@@ -927,6 +930,29 @@ def main():
         ok(lib.GrB_Vector_new(ctypes.byref(qloc), lib.GrB_BOOL, nloc), "qloc")
         ok(lib.GrB_Vector_new(ctypes.byref(q2), lib.GrB_BOOL, n), "q2")
         exchange = gdist.BitmapAllGather(dist, part, world, "cuda")
+    peerx = None
+    exchange_note = None
+    if world > 1 and args.exchange == "peer":
+        # one collective at setup (the windows' IPC handles); none per level.  A setup failure on any
+        # rank, or a self-test exchange that does not assemble the known pattern, falls back to the
+        # all-gather on every rank (the verdict is all-reduced)
+        xdev = "cuda" if args.dist_backend == "nccl" else "cpu"
+        try:
+            peerx = gdist.PeerFrontierExchange(lib, dist, n, world, rank, part, device=xdev)
+            ok_setup = 1
+        except Exception as e:  # noqa: BLE001
+            exchange_note = f"peer window setup failed on rank {rank}: {e}"
+            ok_setup = 0
+        f = torch.tensor([ok_setup], dtype=torch.int64, device=xdev)
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        if f.item() and not peerx.self_test(dist, qloc, q, lo, hi, n, xdev):
+            exchange_note = "peer window self-test failed: all-gather used"
+            f.zero_()
+        if not f.item():
+            if peerx is not None:
+                peerx.free()
+            peerx = None
+            exchange_note = exchange_note or "peer window setup failed on another rank: all-gather used"
     nv = ctypes.c_uint64()
     ev_pairs, level_counts = [], []
 
@@ -937,6 +963,9 @@ def main():
     def exchange_frontier(into_q_bits, qv=None):
         """all-gather the ranks' frontier slices (RCCL, on the library stream) into qv (q)"""
         qv = q if qv is None else qv
+        if peerx is not None:  # device-initiated: put the slice into every window, wait for all
+            peerx.run(qloc, qv)
+            return
         ok(lib.GxB_Vector_bitmap_export(qloc, ctypes.c_void_p(exchange.send.data_ptr()), hi_w - lo_w), "bm out")
         with torch.cuda.stream(stream):
             gath = exchange.run(into_q_bits)  # into_q_bits: straight into q's device bitmap
@@ -995,6 +1024,8 @@ def main():
                 d = sharded_levels_pipelined(timing)
                 level_counts.append(d)
                 return d
+            if peerx is not None:
+                raise SystemExit("--exchange peer runs the pipelined loop only (drop --no-pipeline)")
             if zero_copy:
                 from graphblas_amd import device as gdev
 
@@ -1242,6 +1273,8 @@ def main():
         cpu["graphblas_loop_1thread"] = {"value": done1 / t1_cpu / 1e9, "unit": "GTEPS", "cores": 1,
                                          "sample": f"{runs1} roots, {t1_cpu:.1f} s"}
 
+    if peerx is not None:
+        peerx.check()  # raises if a wait timed out (a peer never arrived): no line is printed then
     if rank == 0:
         out = {
             "metric": "GTEPS (masked mxv/vxm level-BFS, R-MAT s22)",
@@ -1261,7 +1294,10 @@ def main():
                                    f"; GrB_vxm, GrB_mxv on A^T "
                                    f"shards for N>1), R-MAT scale {scale}, edge factor {args.edge_factor}, "
                                    f"16 roots", "n": n, "nnz": nnz,
-                       "parallelism": f"1-D row shards x{world}" if world > 1 else "single GPU"},
+                       "parallelism": (f"1-D row shards x{world}, frontier exchange: "
+                                       f"{'device-initiated peer windows' if peerx else 'all-gather'}"
+                                       + (f" ({exchange_note})" if exchange_note else ""))
+                       if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": (achieved / PEAK_HBM_GBS) if achieved else None, "traffic": traffic,
                          "traffic_source": os.path.relpath(args.traffic_file, ROOT) if traffic else None,
@@ -1284,6 +1320,8 @@ def main():
             "secondary": secondary,
         }
         print(json.dumps(out), flush=True)
+    if peerx is not None:
+        peerx.free()
     if dist:
         dist.barrier()
         dist.destroy_process_group()

@@ -78,6 +78,10 @@ _SIGS = {
     "GxB_Vector_bitmap_export": [P, P, I], "GxB_Vector_bitmap_import": [P, P, I],
     "GxB_Matrix_import_device": [P, P, I, I, P, P, P, I, ctypes.c_bool],
     "GxB_Matrix_colwords_view": [P, P, P], "GxB_Matrix_colwords_touch": [P],
+    # device-initiated frontier exchange (gb_peer.hip)
+    "GxB_PeerWindow_new": [P, I, E, E, P], "GxB_PeerWindow_handle": [P, P], "GxB_PeerWindow_open": [P, E, P],
+    "GxB_PeerWindow_attach": [P, E, P], "GxB_PeerWindow_put": [P, P], "GxB_PeerWindow_wait": [P, P],
+    "GxB_PeerWindow_error": [P, P], "GxB_PeerWindow_free": [P],
     # GrB_Scalar-argument variants (gb_scalar_args.cpp)
     "GrB_Vector_extractElement_Scalar": [P, P, I], "GrB_Matrix_extractElement_Scalar": [P, P, I, I],
     "GrB_Vector_setElement_Scalar": [P, P, I], "GrB_Matrix_setElement_Scalar": [P, P, I, I],

@@ -363,3 +363,171 @@ def pack_bits(mask_bool, nwords):
 def unpack_bits(words, n):
     """int64[*] bitmap words -> bool[n] (numpy)."""
     return np.unpackbits(np.ascontiguousarray(words).view(np.uint8), bitorder="little")[:n].astype(bool)
+
+
+class PeerFrontierExchange:
+    """The per-level frontier exchange of the sharded BFS without a host-issued collective
+    (GxB_PeerWindow_*, csrc/gb_peer.hip): each rank's window -- two frontier
+    bitmaps, per-rank counts and arrival flags, one hipMalloc block -- is exported as an IPC
+    handle, the handles are all-gathered ONCE at setup (the only collective), and every peer
+    maps every window over xGMI.  Per level, put(qloc) writes this rank's slice into all windows
+    and raises its flag in each; wait(q) waits on the device for all flags, assembles q and
+    publishes its count to q's host mailbox (so GxB_Vector_publish_ticket / wait_ticket and
+    GrB_Vector_nvals read it without a stream sync).  Replaces bitmap_export + all-gather +
+    device_touch of the round-5 loop (BitmapAllGather)."""
+
+    HANDLE_BYTES = 64
+
+    def __init__(self, lib, dist, n, world, rank, part, device="cuda"):
+        import ctypes
+
+        import torch
+
+        self.lib, self.world, self.rank = lib, world, rank
+        b = part.get("bounds") or [partition(n, world, k)["lo_w"] for k in range(world)] + [part["words"]]
+        self._bounds = (ctypes.c_uint64 * (world + 1))(*[int(x) for x in b])
+        self.w = ctypes.c_void_p()
+        _ok(lib.GxB_PeerWindow_new(ctypes.byref(self.w), n, world, rank, self._bounds), "GxB_PeerWindow_new")
+        h = (ctypes.c_uint8 * self.HANDLE_BYTES)()
+        _ok(lib.GxB_PeerWindow_handle(h, self.w), "GxB_PeerWindow_handle")
+        mine = torch.tensor(list(bytes(h)), dtype=torch.uint8, device=device)
+        got = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(got, mine)
+        for k in range(world):
+            if k != rank:
+                hk = (ctypes.c_uint8 * self.HANDLE_BYTES)(*got[k].cpu().tolist())
+                _ok(lib.GxB_PeerWindow_open(self.w, k, hk), f"GxB_PeerWindow_open({k})")
+        dist.barrier()
+
+    def self_test(self, dist, qloc, q, lo, hi, n, device):
+        """one exchange of a known pattern (row i set iff i % 7 == 3 or i is a slice end) checked
+        word for word on every rank, the verdicts all-reduced: True when every rank assembled it
+        and no wait timed out.  Leaves qloc and q cleared."""
+        import ctypes
+
+        import torch
+
+        lib = self.lib
+        good = True
+        try:
+            rows = [i - lo for i in range(lo, hi) if i % 7 == 3 or i == hi - 1]
+            for r in rows:
+                _ok(lib.GrB_Vector_setElement_BOOL(qloc, True, r), "setElement")
+            self.run(qloc, q)
+            words = (n + 63) // 64
+            got = torch.zeros(words, dtype=torch.int64, device="cuda")
+            _ok(lib.GxB_Vector_bitmap_export(q, ctypes.c_void_p(got.data_ptr()), words), "bitmap_export")
+            nv = ctypes.c_uint64()
+            _ok(lib.GrB_Vector_nvals(ctypes.byref(nv), q), "nvals")
+            torch.cuda.synchronize()
+            want = np.zeros(n, bool)
+            want[3::7] = True
+            b = self._bounds
+            for k in range(self.world):
+                want[min(n, int(b[k + 1]) * 64) - 1] = int(b[k + 1]) > int(b[k])
+            good = bool(np.array_equal(unpack_bits(got.cpu().numpy(), n), want) and nv.value == int(want.sum()))
+            self.check()
+        except Exception:
+            good = False
+        flag = torch.tensor([1 if good else 0], dtype=torch.int64, device=device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        for v in (qloc, q):
+            lib.GrB_Vector_clear(v)
+        return bool(flag.item())
+
+    def put(self, qloc):
+        _ok(self.lib.GxB_PeerWindow_put(self.w, qloc), "GxB_PeerWindow_put")
+
+    def wait(self, q):
+        _ok(self.lib.GxB_PeerWindow_wait(q, self.w), "GxB_PeerWindow_wait")
+
+    def run(self, qloc, q):
+        self.put(qloc)
+        self.wait(q)
+
+    def check(self):
+        """raises if a wait timed out (a peer never arrived); synchronises the library stream"""
+        import ctypes
+
+        c = ctypes.c_int64()
+        _ok(self.lib.GxB_PeerWindow_error(ctypes.byref(c), self.w), "GxB_PeerWindow_error")
+        if c.value:
+            raise RuntimeError("peer frontier exchange: a peer never arrived (wait timed out)")
+
+    def free(self):
+        import ctypes
+
+        if self.w:
+            self.lib.GxB_PeerWindow_free(ctypes.byref(self.w))
+
+
+def _ok(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with GrB_Info {rc}")
+
+
+class HostPeerWindow:
+    """The peer-window protocol of csrc/gb_peer.hip restated for CPU ranks sharing one host
+    (shared memory instead of xGMI-mapped device memory) -- the exchange of the gloo tests and of
+    CPU-only ranks.  Same layout and order: buf[2][words] by exchange parity, cnt[2][R], flag[R];
+    put(words, count) writes the slice into every window, then the counts, then raises flag[rank]
+    = seq in each (x86 keeps store order); wait() spins until every flag >= seq, then reads
+    buf[seq % 2] and sums cnt[seq % 2].  Two buffers are enough for the pipelined loop: a peer
+    starts exchange seq + 2 only after its wait for seq + 1, which needs this rank's put of
+    seq + 1, which this rank issues after its wait for seq has read buf[seq % 2]."""
+
+    MAXR = 16
+
+    def __init__(self, dist, tag, n, world, rank, bounds=None, timeout=60.0):
+        from multiprocessing import shared_memory
+
+        self.n, self.world, self.rank, self.timeout = n, world, rank, timeout
+        self.words = (n + 63) // 64
+        b = bounds or [partition(n, world, k)["lo_w"] for k in range(world)] + [self.words]
+        self.lo_w, self.hi_w = int(b[rank]), int(b[rank + 1])
+        self.size = (2 * self.words + 2 * self.MAXR + self.MAXR) * 8
+        self._mine = shared_memory.SharedMemory(name=f"{tag}_{rank}", create=True, size=self.size)
+        np.ndarray(self.size // 8, np.uint64, self._mine.buf)[:] = 0
+        dist.barrier()
+        self._shm = [self._mine if k == rank else shared_memory.SharedMemory(name=f"{tag}_{k}")
+                     for k in range(world)]
+        self._views = [self._view(s) for s in self._shm]
+        self.put_seq = self.wait_seq = 0
+        dist.barrier()
+
+    def _view(self, s):
+        a = np.ndarray(self.size // 8, np.uint64, s.buf)
+        w = self.words
+        return {"buf": a[:2 * w].reshape(2, w), "cnt": a[2 * w:2 * w + 2 * self.MAXR].reshape(2, self.MAXR),
+                "flag": a[2 * w + 2 * self.MAXR:]}
+
+    def put(self, slice_words, count):
+        self.put_seq += 1
+        seq, par = self.put_seq, self.put_seq & 1
+        for v in self._views:
+            v["buf"][par, self.lo_w:self.hi_w] = slice_words[:self.hi_w - self.lo_w]
+        for v in self._views:
+            v["cnt"][par, self.rank] = count
+        for v in self._views:
+            v["flag"][self.rank] = seq
+
+    def wait(self):
+        import time
+
+        assert self.wait_seq < self.put_seq, "wait without a put"
+        self.wait_seq += 1
+        seq, par = self.wait_seq, self.wait_seq & 1
+        me = self._views[self.rank]
+        t0 = time.monotonic()
+        while not (me["flag"][:self.world] >= seq).all():
+            if time.monotonic() - t0 > self.timeout:
+                raise RuntimeError("HostPeerWindow: a peer never arrived")
+            time.sleep(0)
+        return me["buf"][par].copy().view(np.int64), int(me["cnt"][par, :self.world].sum())
+
+    def close(self, dist):
+        del self._views
+        dist.barrier()
+        for s in self._shm:
+            s.close()
+        self._mine.unlink()

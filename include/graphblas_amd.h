@@ -431,6 +431,31 @@ GrB_Info GxB_Matrix_colwords_view(uint64_t **words, GrB_Index *nwords, GrB_Matri
  * like GxB_Vector_bitmap_import. */
 GrB_Info GxB_Matrix_colwords_touch(GrB_Matrix A);
 GrB_Info GxB_Vector_bitmap_import(GrB_Vector v, const void *src_device, GrB_Index nwords);
+/* Device-initiated frontier exchange of the 1-D row-sharded level BFS (gb_peer.hip, DESIGN.md
+ * §6): replaces the host-issued all-gather of the frontier slices (GxB_Vector_bitmap_export +
+ * RCCL all-gather + GxB_Vector_device_touch) that follows each shard's GrB_mxv in the
+ * sharded form of reference notebooks/Example B.1 cell 8 (core/matrix.py:2163-2204).
+ * Each rank owns a window (frontier bitmap x 2, per-rank counts and arrival flags) mapped into
+ * every peer: _handle exports it (GxB_PEER_HANDLE_BYTES opaque bytes, hipIpcGetMemHandle), a
+ * peer maps it with _open (hipIpcOpenMemHandle, over xGMI), and several shards driven from one
+ * process link their windows with _attach.  bounds: nranks + 1 offsets in 64-row bitmap words
+ * (NULL: equal slots).  _put(w, qloc) writes the rank's slice qloc (rows [64 bounds[rank],
+ * 64 bounds[rank+1]) of the frontier) into every window and raises the rank's flag there;
+ * _wait(q, w) waits on the device for every rank's flag, assembles the whole frontier in q
+ * (iso true) and publishes its count to q's host mailbox (GxB_Vector_publish_ticket /
+ * wait_ticket, GrB_Vector_nvals) -- no host round trip and no collective per level.  Calls
+ * pair up in order (put, wait, put, wait ...) on every rank.  A peer that never arrives ends
+ * the wait after ~5 s with an empty q; _error then reports 1 (it synchronises the stream). */
+#define GxB_PEER_HANDLE_BYTES 64
+typedef struct GB_PeerWindow_opaque *GxB_PeerWindow;
+GrB_Info GxB_PeerWindow_new(GxB_PeerWindow *w, GrB_Index n, int nranks, int rank, const GrB_Index *bounds);
+GrB_Info GxB_PeerWindow_handle(void *handle, GxB_PeerWindow w);
+GrB_Info GxB_PeerWindow_open(GxB_PeerWindow w, int peer, const void *handle);
+GrB_Info GxB_PeerWindow_attach(GxB_PeerWindow w, int peer, GxB_PeerWindow other);
+GrB_Info GxB_PeerWindow_put(GxB_PeerWindow w, const GrB_Vector qloc);
+GrB_Info GxB_PeerWindow_wait(GrB_Vector q, GxB_PeerWindow w);
+GrB_Info GxB_PeerWindow_error(int64_t *code, GxB_PeerWindow w);
+GrB_Info GxB_PeerWindow_free(GxB_PeerWindow *w);
 /* Build a pattern R-MAT graph on the device (same generator as the oracle):
  * scale, edge factor, seed; values: 0 = BOOL iso true, 1 = INT64 [1,255],
  * 2 = FP64 [0,1); | 0x100 = generate A^T.  Rows [row_begin, row_end) only (row shard),

@@ -237,6 +237,159 @@ def test_sharded_bfs_pipelined_vs_oracle(env, scale, world):
         ok(lib.GrB_Vector_free(ctypes.byref(h)), "free")
 
 
+@pytest.mark.parametrize("scale", [10, 14])
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("balanced", [False, True])
+def test_sharded_bfs_peer_windows_vs_oracle(env, scale, world, balanced):
+    """the sharded loop's exchange without a host-issued collective
+    (GxB_PeerWindow_*, csrc/gb_peer.hip).  Every shard owns a window and its own two frontier
+    buffers; the windows are linked with GxB_PeerWindow_attach (the same mapping an IPC-opened
+    peer window gives, here inside one process and one GPU); per level every shard's GrB_mxv is
+    followed by GxB_PeerWindow_put of its slice into every window, then GxB_PeerWindow_wait
+    assembles each shard's full frontier on the device and publishes its count -- read through
+    a publish ticket one level behind (dist.pipelined_levels).  Levels bit-exact vs the oracle,
+    every shard's frontier equal, and no wait timed out."""
+    gb, torch, stream = env
+    from graphblas_amd import dist as gdist
+
+    lib = gb.lib
+    n = 1 << scale
+    G = O.rmat(scale, 16, 42)
+    deg = np.diff(G.indptr)
+    bounds = None
+    if balanced:  # 1-D row blocks balanced by the A^T shards' entries (in-degrees)
+        words = (n + 63) // 64
+        din = np.zeros(words * 64, np.int64)
+        din[:n] = np.bincount(G.indices, minlength=n)
+        bounds = gdist.balanced_bounds(din.reshape(words, 64).sum(1), world)
+    parts = [gdist.partition(n, world, r, bounds) for r in range(world)]
+    bvec = [p["lo_w"] for p in parts] + [parts[0]["words"]]
+    AT, v, ql, win = [], [], [], []
+    qb = [[], []]
+    for r, p in enumerate(parts):
+        nloc = p["hi"] - p["lo"]
+        h = ctypes.c_void_p()
+        ok(lib.GxB_Matrix_rmat(ctypes.byref(h), scale, 16, 42, 0x100, 0, p["lo"], p["hi"]), "rmat shard")
+        AT.append(h)
+        for lst, t, sz in ((v, lib.GrB_INT32, nloc), (ql, lib.GrB_BOOL, nloc), (qb[0], lib.GrB_BOOL, n),
+                           (qb[1], lib.GrB_BOOL, n)):
+            x = ctypes.c_void_p()
+            ok(lib.GrB_Vector_new(ctypes.byref(x), t, sz), "new")
+            lst.append(x)
+        w = ctypes.c_void_p()
+        ok(lib.GxB_PeerWindow_new(ctypes.byref(w), n, world, r, (ctypes.c_uint64 * (world + 1))(*bvec)), "window")
+        win.append(w)
+    for r in range(world):
+        for k in range(world):
+            if k != r:
+                ok(lib.GxB_PeerWindow_attach(win[r], k, win[k]), "attach")
+    sr = lib.GxB_ANY_PAIR_BOOL
+
+    def exchange(tgt):
+        for r in range(world):
+            ok(lib.GxB_PeerWindow_put(win[r], ql[r]), "put")
+        for r in range(world):
+            ok(lib.GxB_PeerWindow_wait(qb[tgt][r], win[r]), "wait")
+        t = ctypes.c_uint64()
+        ok(lib.GxB_Vector_publish_ticket(ctypes.byref(t), qb[tgt][0]), "ticket")
+        return qb[tgt][0], t.value
+
+    rng = np.random.default_rng(scale + 10 * world)
+    for src in [int(np.argmax(deg)), int(rng.choice(np.flatnonzero(deg > 0)))]:
+        for x in v + ql:
+            ok(lib.GrB_Vector_clear(x), "clear")
+        for r, p in enumerate(parts):
+            if p["lo"] <= src < p["hi"]:
+                ok(lib.GrB_Vector_setElement_BOOL(ql[r], True, src - p["lo"]), "root")
+        exchange(0)
+        issued = []
+
+        def enqueue(d):
+            issued.append(d)
+            for r, p in enumerate(parts):
+                ok(lib.GrB_Vector_assign_INT32(v[r], ql[r], None, d, lib.GrB_ALL, p["hi"] - p["lo"], None), "assign")
+            for r in range(world):
+                ok(lib.GrB_mxv(ql[r], v[r], None, sr, AT[r], qb[(d - 1) % 2][r], lib.GrB_DESC_RSC), "mxv")
+            return exchange(d % 2)
+
+        def count_of(tok):
+            c = ctypes.c_uint64()
+            ok(lib.GxB_Vector_wait_ticket(ctypes.byref(c), tok[0], ctypes.c_uint64(tok[1])), "wait ticket")
+            return c.value
+
+        nlev = gdist.pipelined_levels(enqueue, count_of, max_levels=n + 2)
+        got = np.zeros(n, np.int32)
+        for r, p in enumerate(parts):
+            idx, lv = _extract_int32(lib, v[r])
+            got[idx + p["lo"]] = lv
+        lev, _, _ = O.bfs_levels(G, src)
+        assert np.array_equal(got, lev), f"source {src}"
+        assert nlev == int(lev.max()) and issued == list(range(1, nlev + 2))
+        # every shard assembled the same (empty) last frontier
+        for r in range(world):
+            nv = ctypes.c_uint64()
+            ok(lib.GrB_Vector_nvals(ctypes.byref(nv), qb[nlev % 2][r]), "nvals")
+            assert nv.value == 0
+    # a mid-BFS frontier is the same on every shard (the bitmaps, word for word)
+    from graphblas_amd import device as gdev
+    ok(lib.GrB_Vector_clear(ql[0]), "clear")
+    for r in range(1, world):
+        ok(lib.GrB_Vector_clear(ql[r]), "clear")
+    p0 = parts[0]
+    for i in range(0, p0["hi"] - p0["lo"], 3):
+        ok(lib.GrB_Vector_setElement_BOOL(ql[0], True, i), "set")
+    exchange(1)
+    torch.cuda.synchronize()
+    ref = gdev.device_tensor(torch, gdev.vector_view(qb[1][0]).bitmap, parts[0]["words"]).cpu()
+    for r in range(1, world):
+        assert torch.equal(gdev.device_tensor(torch, gdev.vector_view(qb[1][r]).bitmap, parts[0]["words"]).cpu(), ref)
+    for r in range(world):
+        e = ctypes.c_int64()
+        ok(lib.GxB_PeerWindow_error(ctypes.byref(e), win[r]), "error")
+        assert e.value == 0
+        ok(lib.GxB_PeerWindow_free(ctypes.byref(win[r])), "free window")
+    for h in AT:
+        ok(lib.GrB_Matrix_free(ctypes.byref(h)), "free")
+    for h in v + ql + qb[0] + qb[1]:
+        ok(lib.GrB_Vector_free(ctypes.byref(h)), "free")
+
+
+def test_peer_window_wait_times_out_instead_of_hanging(env):
+    """a wait whose peer never puts ends after the timeout (knob peer_timeout_ms) with an empty
+    frontier and the window's error word raised -- the kernel does not spin forever"""
+    gb, torch, stream = env
+    lib = gb.lib
+    n = 1 << 10
+    w = [ctypes.c_void_p(), ctypes.c_void_p()]
+    for r in range(2):
+        ok(lib.GxB_PeerWindow_new(ctypes.byref(w[r]), n, 2, r, None), "window")
+    ok(lib.GxB_PeerWindow_attach(w[0], 1, w[1]), "attach")
+    ok(lib.GxB_PeerWindow_attach(w[1], 0, w[0]), "attach")
+    ql, q = ctypes.c_void_p(), ctypes.c_void_p()
+    ok(lib.GrB_Vector_new(ctypes.byref(ql), lib.GrB_BOOL, n // 2), "ql")
+    ok(lib.GrB_Vector_new(ctypes.byref(q), lib.GrB_BOOL, n), "q")
+    ok(lib.GrB_Vector_setElement_BOOL(ql, True, 3), "set")
+    try:
+        ok(lib.GxB_Global_set_int(b"peer_timeout_ms", 50), "knob")
+        ok(lib.GxB_PeerWindow_put(w[0], ql), "put")  # rank 1 never puts
+        ok(lib.GxB_PeerWindow_wait(q, w[0]), "wait")
+        nv = ctypes.c_uint64()
+        ok(lib.GrB_Vector_nvals(ctypes.byref(nv), q), "nvals")
+        assert nv.value == 0
+        e = ctypes.c_int64()
+        ok(lib.GxB_PeerWindow_error(ctypes.byref(e), w[0]), "error")
+        assert e.value == 1
+        # misuse is refused on the host: a wait without its put, a slice of the wrong size
+        assert lib.GxB_PeerWindow_wait(q, w[1]) == lib.GrB_INVALID_VALUE
+        assert lib.GxB_PeerWindow_put(w[1], q) == lib.GrB_DIMENSION_MISMATCH
+    finally:
+        lib.GxB_Global_set_int(b"peer_timeout_ms", 0)
+        for r in range(2):
+            lib.GxB_PeerWindow_free(ctypes.byref(w[r]))
+        lib.GrB_Vector_free(ctypes.byref(ql))
+        lib.GrB_Vector_free(ctypes.byref(q))
+
+
 @pytest.mark.parametrize("scale", [10, 13])
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("k", [7, 64])
