@@ -149,12 +149,28 @@ static inline bool slot_match(gb_host_slot *s, uint64_t seq, int64_t *value) {
     return false;
 }
 
+// The stream is asked whether it drained (a publish that never lands: a failed launch) only once
+// the wait has lasted `slot_query_us` (default 2000 us, longer than any level's kernel): each
+// hipStreamQuery on a busy stream makes the runtime put a marker into the queue behind the
+// enqueued kernels, and the GPU then idles ~3.5 us between them (tools/iso_gaps.py: the BFS
+// levels after a long wait started 6 us after the previous one ended instead of 2.5 us when the
+// query ran every 1024 spins, i.e. on every wait longer than ~40 us).
 bool gb_host_slot_wait(gb_host_slot *s, uint64_t seq, int64_t *value) {
+    int64_t t0 = 0, query_ns = 0;
     for (uint64_t i = 1;; i++) {
         if (slot_match(s, seq, value)) return true;
         if ((i & 1023) == 0) {
-            hipError_t q = hipStreamQuery(gb_stream_peek());
-            if (q != hipErrorNotReady) return slot_match(s, seq, value);  // drained (or failed): one last look
+            const int64_t now = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                    std::chrono::steady_clock::now().time_since_epoch()).count();
+            if (!t0) {
+                t0 = now;
+                const int64_t k = gb_knob("slot_query_us");
+                query_ns = (k > 0 ? k : 2000) * 1000;
+            }
+            if (now - t0 >= query_ns) {
+                hipError_t q = hipStreamQuery(gb_stream_peek());
+                if (q != hipErrorNotReady) return slot_match(s, seq, value);  // drained (or failed): one last look
+            }
         }
         __builtin_ia32_pause();
     }
@@ -393,6 +409,8 @@ int64_t gb_read_i64(const int64_t *dptr) {
     return v;
 }
 
+int64_t gb_iso_ts_dump();  // gb_mxv.hip (diagnostics)
+
 static const char *k_type_names[] = {"BOOL", "INT8", "UINT8", "INT16", "UINT16", "INT32",
                                      "UINT32", "INT64", "UINT64", "FP32", "FP64"};
 static const size_t k_type_sizes[] = {1, 1, 1, 2, 2, 4, 4, 8, 8, 4, 8};
@@ -508,6 +526,9 @@ GrB_Info GxB_Global_get_int(const char *key, int64_t *value) {
     if (!strcmp(key, "stat_nvals_copy")) {
         *value = g_stat_nvals_copy.load(std::memory_order_relaxed);
         return GrB_SUCCESS;
+    }
+    if (!strcmp(key, "iso_ts_dump")) {  // diagnostics: GRAPHBLAS_AMD_ISO_TS (gb_mxv.hip)
+        return gb_api(nullptr, [&] { *value = gb_iso_ts_dump(); });
     }
     // named kernel-class counters (gb_stat_add): "stat_" + name; 0 before the first count
     if (!strncmp(key, "stat_", 5)) {

@@ -782,6 +782,10 @@ struct gb_iso_args {
     const void *asg_qiso;
     int asg_qiso_code;
     unsigned long long *asg_count;
+    // diagnostics (environment GRAPHBLAS_AMD_ISO_TS): wall-clock stamps (s_memrealtime, 100 MHz) of
+    // each launch's start (block 0) and end (the finishing block), ts[0] / ts[1] launch counters,
+    // pairs from ts[2] -- kernel gaps without a profiler (tools/iso_gaps.py)
+    unsigned long long *ts;
 };
 
 // ------------------------------------------------ general SpMV: balanced words
@@ -1196,7 +1200,16 @@ __global__ void k_spmv_fold(SR sr, const int32_t *__restrict__ chunks, int64_t n
 #define ISO_VAL_BITS 27
 
 // hand the count to the host without a copy (gb_host_slot_wait)
+#define ISO_TS_PAIRS (1 << 20)
+__device__ __forceinline__ void iso_ts_mark(const gb_iso_args &a, int which) {
+    if (!a.ts) return;
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long k = atomicAdd(&a.ts[which], 1ULL);
+    if (k < ISO_TS_PAIRS) a.ts[2 + 2 * k + which] = t;
+}
+
 __device__ __forceinline__ void iso_publish(const gb_iso_args &a, long long tot) {
+    iso_ts_mark(a, 1);
     if (!a.pub || (a.dbg & 1)) return;
     if (a.pub_form == 1) {
         __hip_atomic_store(&a.pub->value, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1280,6 +1293,7 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
     unsigned long long *__restrict__ tcount, unsigned long long *__restrict__ gst, gb_iso_args a) {
     __shared__ gb_wlist lists[WAVES_PER_BLOCK];
     gb_wlist &L = lists[threadIdx.x >> 6];
+    if (a.ts && blockIdx.x == 0 && threadIdx.x == 0) iso_ts_mark(a, 0);
     if (a.dbg & 8) return;  // diagnostics: the launch alone
     bool push = false;
     if (a.host_dir == 1) {
@@ -1538,6 +1552,34 @@ static bool idempotent_monoid(int m) {
 }
 
 static std::mutex g_dir_mu;
+static unsigned long long *g_iso_ts = nullptr;  // GRAPHBLAS_AMD_ISO_TS diagnostics buffer
+static unsigned long long *iso_ts_buffer() {
+    static const bool on = getenv("GRAPHBLAS_AMD_ISO_TS") != nullptr;
+    if (!on) return nullptr;
+    if (!g_iso_ts) {
+        GB_HIP(hipMalloc((void **)&g_iso_ts, (2 + 2 * (size_t)ISO_TS_PAIRS) * sizeof(unsigned long long)));
+        GB_HIP(hipMemset(g_iso_ts, 0, (2 + 2 * (size_t)ISO_TS_PAIRS) * sizeof(unsigned long long)));
+        GB_HIP(hipDeviceSynchronize());
+    }
+    return g_iso_ts;
+}
+// writes the stamps to the file GRAPHBLAS_AMD_ISO_TS names (raw u64: starts, ends, pairs); returns the
+// launch count (GxB_Global_get_int("iso_ts_dump"))
+int64_t gb_iso_ts_dump() {
+    const char *path = getenv("GRAPHBLAS_AMD_ISO_TS");
+    if (!path || !g_iso_ts) return 0;
+    GB_HIP(hipStreamSynchronize(gb_stream()));
+    unsigned long long c[2];
+    GB_HIP(hipMemcpy(c, g_iso_ts, sizeof(c), hipMemcpyDeviceToHost));
+    const size_t k = std::min<unsigned long long>(std::min(c[0], c[1]), ISO_TS_PAIRS);
+    std::vector<unsigned long long> buf(2 + 2 * k);
+    GB_HIP(hipMemcpy(buf.data(), g_iso_ts, buf.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    FILE *f = fopen(path, "wb");
+    if (!f) return -1;
+    fwrite(buf.data(), sizeof(unsigned long long), buf.size(), f);
+    fclose(f);
+    return (int64_t)k;
+}
 static uint64_t *g_spare = nullptr;  // zeroed bitmap for the next iso SpMV's output (under g_dir_mu)
 static int64_t g_spare_words = 0;
 
@@ -1653,6 +1695,7 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
                 args.asg_count = (unsigned long long *)asg->count;
             }
             args.dbg = (int)gb_knob("iso_dbg");
+            args.ts = iso_ts_buffer();
             args.packed = n < (1LL << ISO_VAL_BITS) && u.n < (1LL << ISO_VAL_BITS) && gb_knob("iso_packed") != 1;
             if (args.dbg & 1) T.pub = nullptr;  // diagnostics: the host reads the count by a copy
             // lane-per-row steps after the pull heads: none by default (tools/gpu_ab2.sh, s22
