@@ -188,6 +188,21 @@ struct gb_spec_hold_guard {
     gb_spec_hold_guard() { g_spec_hold++; }
     ~gb_spec_hold_guard() { g_spec_hold--; }
 };
+// A pending root (gb_object.hip): `GrB_Vector_setElement_BOOL(q, true, i)` on an empty BOOL vector
+// -- the BFS start, notebooks/Example B.1 cell 8 -- is recorded instead of launched; the level
+// SpMV of the notebook shape that reads q consumes it (its kernel pushes from vertex i, gb_mxv.hip
+// gb_push_root), and the deferred stamp `v<q> = 1` before it keeps it pending (g_root_hold); any
+// other API call materialises it first (gb_root_flush: the single-thread set launch it replaced).
+extern std::atomic<bool> g_root_active;
+extern thread_local int g_root_hold;
+void gb_root_flush();
+bool gb_root_pending(const GB_Obj *v);
+int64_t gb_root_take(GB_Obj *v);  // the root index, the record cleared; -1 when v holds none
+const void *gb_bool_true_dev();   // one device byte holding true (a consumed root's iso value)
+struct gb_root_hold_guard {
+    gb_root_hold_guard() { g_root_hold++; }
+    ~gb_root_hold_guard() { g_root_hold--; }
+};
 
 // roctx ranges named by the API entry point around each library call (environment
 // GRAPHBLAS_AMD_ROCTX=1; the roctx library is loaded then, never otherwise), so a rocprofv3
@@ -211,6 +226,7 @@ GrB_Info gb_api_impl(GB_Obj *errobj, F &&body, const char *name = nullptr) {
     gb_roctx_range range(name);
     try {
         if (FLUSH && !g_spec_hold && g_spec_active.load(std::memory_order_acquire)) gb_spec_resolve(nullptr);
+        if (FLUSH && !g_root_hold && g_root_active.load(std::memory_order_acquire)) gb_root_flush();
         if (FLUSH && g_pending_active.load(std::memory_order_acquire)) gb_pending_flush();
         body();
         if (errobj && errobj->magic == GB_MAGIC) errobj->err.clear();
@@ -525,6 +541,8 @@ struct gb_asg {
     // u's device count is exact (written by the kernel that produced u, earlier on the stream):
     // an empty u ends the launch early (the speculated level after a BFS's last one)
     bool u_count_exact = false;
+    // u is a pending root (gb_root_take): the frontier is {root}; u's storage does not hold it
+    int64_t root = -1;
 };
 void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, gb_bitmap_view &u,
              const gb_vmask &mask, GrB_Semiring sr, bool flip, const gb_asg *asg = nullptr);

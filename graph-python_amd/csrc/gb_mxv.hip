@@ -198,7 +198,8 @@ __device__ __forceinline__ long long gb_push_targets(const int32_t (&j)[4], bool
                                                      const uint64_t *__restrict__ mbits, bool mcomp,
                                                      unsigned long long *__restrict__ tbits,
                                                      const int64_t *__restrict__ hprow, long long &mfn,
-                                                     const uint64_t *__restrict__ qbits, bool serial = false) {
+                                                     const uint64_t *__restrict__ qbits, bool serial = false,
+                                                     int64_t qroot = -1) {
     unsigned long long cur[4];
     if (serial) {  // diagnostics (iso_dbg 128): the round-4 order, each read behind the one before
         if (mbits) {
@@ -223,9 +224,10 @@ __device__ __forceinline__ long long gb_push_targets(const int32_t (&j)[4], bool
             }
         }
         if (mbits) {
+            // qroot: the fused stamp's frontier is one pending vertex (gb_push_root), not q's bits
 #pragma unroll
             for (int u = 0; u < 4; u++)
-                if (ok[u]) ok[u] = ((((mw[u] | qw[u]) >> (j[u] & 63)) & 1ULL) != 0) != mcomp;
+                if (ok[u]) ok[u] = (((((mw[u] | qw[u]) >> (j[u] & 63)) & 1ULL) != 0) || j[u] == qroot) != mcomp;
         }
     }
     long long added = 0;
@@ -449,6 +451,41 @@ __device__ __forceinline__ long long gb_push_phase(int64_t nwords_u, const uint6
             added += gb_push_targets(j, ok, mbits, mcomp, tbits, hprow, mfn, qbits, serial);
         }
         gb_wave_sync();
+    }
+    return added;
+}
+
+// Push from a single pending vertex (the BFS root, gb_internal.h g_root_active): the host knows
+// the frontier is {root}, so the kernel neither tests the hub table against the frontier nor
+// scans its bitmap words (which do not hold the root) -- the root's edges are spread over the
+// whole grid, 4 per lane per step, and block 0 carries out the fused stamp v<q> = x for it.
+// Replaces the single-thread set launch and the first level's two scan round trips.
+__device__ __forceinline__ long long gb_push_root(int64_t root, const int64_t *__restrict__ prow,
+                                                 const int32_t *__restrict__ pcol,
+                                                 const uint64_t *__restrict__ mbits, bool mcomp,
+                                                 unsigned long long *__restrict__ tbits,
+                                                 const int64_t *__restrict__ hprow, long long &mfn, bool stamp,
+                                                 const gb_asg_dev &g, long long &adelta) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    if (stamp && blockIdx.x == 0 && threadIdx.x == 0) {
+        const unsigned long long m = 1ULL << (root & 63);
+        const unsigned long long old = atomicOr((unsigned long long *)&g.bits[root >> 6], m);
+        gb_store_sized(g.vals, root, g.size, g.x);
+        if (!(old & m)) adelta += 1;
+    }
+    const int64_t p0 = prow[root], p1 = prow[root + 1];
+    long long added = 0;
+    for (int64_t p = p0 + wave * 256 + lane; p < p1; p += nwaves * 256) {
+        int32_t j[4];
+        bool ok[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            ok[u] = p + 64 * u < p1;
+            j[u] = ok[u] ? pcol[p + 64 * u] : 0;
+        }
+        added += gb_push_targets(j, ok, mbits, mcomp, tbits, hprow, mfn, nullptr, false, stamp ? root : -1);
     }
     return added;
 }
@@ -782,6 +819,7 @@ struct gb_iso_args {
     const void *asg_qiso;
     int asg_qiso_code;
     unsigned long long *asg_count;
+    int64_t root;  // >= 0: the frontier is this one pending vertex (gb_push_root); u's bits do not hold it
     // diagnostics (environment GRAPHBLAS_AMD_ISO_TS): wall-clock stamps (s_memrealtime, 100 MHz) of
     // each launch's start (block 0) and end (the finishing block), ts[0] / ts[1] launch counters,
     // pairs from ts[2] -- kernel gaps without a profiler (tools/iso_gaps.py)
@@ -1343,6 +1381,9 @@ __global__ __launch_bounds__(SPMV_BLOCK) void k_iso_work(
     long long mfn = 0, cnt = 0, adelta = 0;
     if (a.dbg & 4)
         ;
+    else if (a.root >= 0)
+        cnt = gb_push_root(a.root, prow, pcol, mbits, mcomp, (unsigned long long *)tbits, a.hprow, mfn,
+                           a.asg.bits != nullptr, a.asg, adelta);
     else if (push)
         cnt = gb_push_phase(nwords_u, ubits, prow, pcol, hubs, nhubs, H, mbits, mcomp,
                             (unsigned long long *)tbits, L, a.hprow, mfn, qbits, a.asg, adelta, (a.dbg & 128) != 0,
@@ -1696,6 +1737,8 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             }
             args.dbg = (int)gb_knob("iso_dbg");
             args.ts = iso_ts_buffer();
+            args.root = asg ? asg->root : -1;
+            GB_REQUIRE(args.root < 0 || can_push, GrB_PANIC, "a pending root needs the push orientation");
             args.packed = n < (1LL << ISO_VAL_BITS) && u.n < (1LL << ISO_VAL_BITS) && gb_knob("iso_packed") != 1;
             if (args.dbg & 1) T.pub = nullptr;  // diagnostics: the host reads the count by a copy
             // lane-per-row steps after the pull heads: none by default (tools/gpu_ab2.sh, s22
@@ -1740,7 +1783,8 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
             g_spare = nullptr;
             g_spare_words = 0;
             args.out_zeroed = spare_taken;
-            if (asg && asg->u_count_exact && u.count && gb_knob("spec_empty_exit") != 1) args.u_exit = u.count;
+            if (asg && asg->u_count_exact && u.count && asg->root < 0 && gb_knob("spec_empty_exit") != 1)
+                args.u_exit = u.count;
             bool need_prep = false;
             if (can_push) {
                 units = std::max<int64_t>(units, std::max<int64_t>((Apush->nhubs + 15) / 16, (uw + 3) / 4));
@@ -1772,7 +1816,15 @@ void gb_spmv(gb_vec_result &T, const gb_csr_view &A, const gb_csr_view *Apush, g
                     push_sure = open_lo >= 0 &&
                                 (double)u.h_nvals * (double)Apush->maxdeg * (double)alpha < (double)open_lo * avg;
                 }
-                if (hint_ok && spare_taken) {
+                if (args.root >= 0) {
+                    // the frontier is one vertex the host knows; the push writes T's bitmap directly, so
+                    // it must start zeroed (the spare usually is; a first call zeroes it here)
+                    if (!spare_taken) gb_memset(T.bits, 0, nw * sizeof(uint64_t));
+                    args.out_zeroed = true;
+                    args.host_dir = 1;
+                    g_stat_host_push.fetch_add(1, std::memory_order_relaxed);
+                    gb_stat_add("bfs_root_push", 1);
+                } else if (hint_ok && spare_taken) {
                     args.mf_hint = u.mf_hint;  // decide in the work kernel: one launch
                 } else if (push_sure) {
                     args.host_dir = 1;  // one launch, no prep

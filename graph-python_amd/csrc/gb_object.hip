@@ -10,6 +10,8 @@
 #include <vector>
 
 #include "gb_device.cuh"
+#include <mutex>
+
 #include "gb_internal.h"
 
 #define GB_BLOCK 256
@@ -791,9 +793,66 @@ __global__ void k_vec_clear(unsigned long long *__restrict__ bits, int64_t i, un
     if (old & m) atomicAdd(cnt, (unsigned long long)-1LL);
 }
 
+// ---- the pending root (gb_internal.h)
+std::atomic<bool> g_root_active{false};
+thread_local int g_root_hold = 0;
+static std::mutex g_root_mu;
+static GB_Obj *g_root_v = nullptr;
+static int64_t g_root_i = -1;
+
+void gb_root_flush() {
+    std::lock_guard<std::mutex> lk(g_root_mu);
+    GB_Obj *v = g_root_v;
+    g_root_v = nullptr;
+    g_root_active.store(false, std::memory_order_release);
+    if (!v || v->magic != GB_MAGIC) return;
+    hipLaunchKernelGGL(k_vec_set<bool>, dim3(1), dim3(1), 0, gb_stream(), (unsigned long long *)v->bits, nullptr,
+                       g_root_i, true, (unsigned long long *)v->d_nvals, (bool *)v->dense);
+    GB_LAUNCH_CHECK();
+}
+bool gb_root_pending(const GB_Obj *v) {
+    if (!g_root_active.load(std::memory_order_acquire)) return false;
+    std::lock_guard<std::mutex> lk(g_root_mu);
+    return v && v == g_root_v;
+}
+int64_t gb_root_take(GB_Obj *v) {
+    std::lock_guard<std::mutex> lk(g_root_mu);
+    if (!v || v != g_root_v) return -1;
+    g_root_v = nullptr;
+    g_root_active.store(false, std::memory_order_release);
+    return g_root_i;
+}
+const void *gb_bool_true_dev() {
+    static std::mutex mu;
+    static bool *p = nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!p) {
+        GB_HIP(hipMalloc((void **)&p, 16));
+        const unsigned char one[16] = {1};
+        GB_HIP(hipMemcpy(p, one, sizeof(one), hipMemcpyHostToDevice));
+    }
+    return p;
+}
+
 template <class T>
 static void vector_set_element(GB_Obj *v, T x, int64_t i) {
     GB_REQUIRE(i >= 0 && i < v->nrows, GrB_INVALID_INDEX, "index out of range");
+    if constexpr (std::is_same<T, bool>::value) {
+        // the first entry of an empty BOOL vector, true: deferred (the BFS root; gb_internal.h)
+        if (x && v->kind == GB_KIND_VECTOR && v->type->code == GBAMD_T_BOOL && v->nvals_valid && v->nvals == 0 &&
+            !v->dense && v->bits && v->invalid == GrB_SUCCESS && gb_knob("root_defer") != 1) {
+            if (g_root_active.load(std::memory_order_acquire)) gb_root_flush();  // one record at a time
+            v->dense = gb_malloc(sizeof(bool));  // written when the root materialises (or never read)
+            v->iso = true;
+            v->nvals = 1;  // known on the host
+            v->hint_valid = false;
+            std::lock_guard<std::mutex> lk(g_root_mu);
+            g_root_v = v;
+            g_root_i = i;
+            g_root_active.store(true, std::memory_order_release);
+            return;
+        }
+    }
     T *iso_init = nullptr;
     if (!v->dense) {
         // first value: store it as an iso vector (the set kernel writes the value)

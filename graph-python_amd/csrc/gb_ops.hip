@@ -115,12 +115,31 @@ static void do_spmv(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, GrB_Semiring sr
     if (g_pending_active.load(std::memory_order_acquire)) {
         fused = A->kind == GB_KIND_MATRIX && u->kind != GB_KIND_MATRIX &&
                 take_pending_assign(asg, w, mask, A, u, d, gb_spmv_result_iso(sr, A->iso, u->iso, vxm));
-        if (!fused) gb_pending_flush();
+        if (!fused) {
+            if (g_root_active.load(std::memory_order_acquire)) gb_root_flush();  // the assign may read it
+            gb_pending_flush();
+        }
     }
     const int64_t hp_t0 = g_hprof_on ? gb_hprof_now() : 0;
     spmv_views V;
     spmv_build_views(V, mask, sr, A, u, d, vxm, a_rows, fused ? &asg : nullptr);
     if (g_hprof_on) gb_hprof_add(2, "do_spmv views+mask", gb_hprof_now() - hp_t0);
+    // a pending root (the BFS start): consumed by the notebook level shape -- q<!v.S, replace> =
+    // q (+).(x) A with the stamp v<q> = x fused, iso result, push orientation at hand -- whose kernel
+    // pushes from it; materialised before any other SpMV
+    if (g_root_active.load(std::memory_order_acquire)) {
+        const bool shape = fused && u == w && !accum && d.replace && d.comp && d.structure && V.iso_result &&
+                           V.push && V.push->nrows == u->nrows && V.push->hubs && gb_knob("spmv_direction") != 1;
+        if (shape) asg.root = gb_root_take(u);
+        if (asg.root >= 0) {
+            // u's storage does not hold the root: its iso value (true) and count come from the host
+            V.uv.vals = gb_bool_true_dev();
+            V.uv.count = nullptr;
+            if (asg.q_iso) asg.q_iso = gb_bool_true_dev();
+        } else {
+            gb_root_flush();
+        }
+    }
     gb_vec_result T;
     if (w->kind != GB_KIND_MATRIX) {
         if (!w->pub) w->pub = gb_host_slot_alloc();
@@ -652,6 +671,8 @@ static struct {
 // goes on.  The pending record is cleared only once the assign has been issued or has
 // failed and been recorded.
 void gb_pending_flush() {
+    // the assign reads its mask's (or writes its target's) storage: a pending root there is materialised
+    if (g_root_active.load(std::memory_order_acquire)) gb_root_flush();
     std::lock_guard<std::mutex> lk(g_pend_mu);
     GB_Obj *w = g_pend.w, *m = g_pend.mask;
     if (w && w->magic == GB_MAGIC && m && m->magic == GB_MAGIC && w->invalid == GrB_SUCCESS) {
@@ -1002,7 +1023,12 @@ static void vector_assign_scalar(GB_Obj *w, GB_Obj *mask, GrB_BinaryOp accum, co
             memcpy(xc, &dv, sizeof(D));
         });
     });
+    // a pending root stays pending only under the deferred stamp whose mask it is (gb_internal.h)
+    if (g_root_active.load(std::memory_order_acquire) &&
+        !(I == GrB_ALL && !accum && mask && gb_root_pending(mask) && !gb_root_pending(w)))
+        gb_root_flush();
     if (I == GrB_ALL && !accum && try_defer_assign(w, mask, xc, d)) return;
+    if (g_root_active.load(std::memory_order_acquire)) gb_root_flush();  // not deferred: the assign reads it
     if (I == GrB_ALL && !accum && assign_all_scalar_fast(w, mask, xc, d)) return;
     gb_vec_result T;
     scalar_vec_T(T, w->nrows, I, ni, xc, ct);
@@ -1505,6 +1531,7 @@ GrB_Info GrB_Semiring_new(GrB_Semiring *semiring, GrB_Monoid add, GrB_BinaryOp m
     GrB_Info GrB_Vector_assign_##T(GrB_Vector w, const GrB_Vector mask, const GrB_BinaryOp accum, ctype x,   \
                                    const GrB_Index *I, GrB_Index ni, const GrB_Descriptor desc) {            \
         GB_HPROF(8, "GrB_Vector_assign scalar");                                                             \
+        gb_root_hold_guard root_hold; /* a deferred stamp whose mask is a pending root keeps it pending */   \
         if (g_spec_active.load(std::memory_order_acquire) && w && OBJ(w)->magic == GB_MAGIC) {             \
             /* the predicted level stamp, already carried out (BFS speculation); the match runs   \
                inside the API wrapper so that nothing it raises crosses the C boundary */          \
