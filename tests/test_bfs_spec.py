@@ -400,3 +400,86 @@ def test_value_mask_false_entries_no_host_push(gb, graph):
         assert stat(gb, "stat_spmv_host_push") == h1
     for x in (u, m, w):
         lib.GrB_Vector_free(ctypes.byref(x))
+
+
+def test_pending_root_is_unobservable(gb, graph):
+    """`GrB_Vector_setElement_BOOL(q, true, src)` on an empty BOOL vector stays
+    pending (no launch) and the first level's kernel pushes from src (gb_push_root; counter
+    stat_bfs_root_push).  Every other use of q sees the entry: its count and tuples, q as a mask,
+    q as the input of an SpMV of another shape, an assign into q, a second setElement -- each
+    against the same calls with the deferral off (knob root_defer = 1) and the numpy loop."""
+    G, A = graph
+    n = G.nrows
+    lib = gb.lib
+    src = int(roots(G)[1])
+    sr = lib.GxB_ANY_PAIR_BOOL
+    nv = U64()
+
+    def fresh(t=lib.GrB_BOOL):
+        x = ctypes.c_void_p()
+        ok(lib.GrB_Vector_new(ctypes.byref(x), t, n))
+        return x
+
+    def bits(x):
+        ok(lib.GrB_Vector_nvals(ctypes.byref(nv), x))
+        idx = np.empty(nv.value, np.uint64)
+        val = np.empty(nv.value, np.bool_)
+        ok(lib.GrB_Vector_extractTuples_BOOL(ctypes.c_void_p(idx.ctypes.data), ctypes.c_void_p(val.ctypes.data),
+                                             ctypes.byref(nv), x))
+        return sorted(idx.astype(np.int64).tolist()), val.tolist()
+
+    succ = sorted(set(G.indices[G.indptr[src]:G.indptr[src + 1]].tolist()))
+    results = []
+    for knob in (0, 1):
+        gb.set_knob("root_defer", knob)
+        try:
+            out = {}
+            q = fresh()
+            ok(lib.GrB_Vector_setElement_BOOL(q, True, src))
+            out["tuples"] = bits(q)
+            q2 = fresh()
+            ok(lib.GrB_Vector_setElement_BOOL(q2, True, src))
+            w = fresh()  # another shape: w = q2 any.pair A, no mask, w != q2
+            ok(lib.GrB_vxm(w, None, None, sr, q2, A._carg, None), "vxm other shape")
+            out["vxm_other"] = bits(w)[0]
+            q3 = fresh()
+            m = fresh()
+            ok(lib.GrB_Vector_setElement_BOOL(q3, True, src))
+            ok(lib.GrB_Vector_assign_BOOL(m, q3, None, True, lib.GrB_ALL, n, None), "q3 as a mask")
+            out["as_mask"] = bits(m)[0]
+            q4 = fresh()
+            ok(lib.GrB_Vector_setElement_BOOL(q4, True, src))
+            ok(lib.GrB_Vector_setElement_BOOL(q4, True, (src + 1) % n), "a second entry")
+            out["two"] = bits(q4)[0]
+            q5 = fresh()
+            v5 = fresh(lib.GrB_INT32)
+            ok(lib.GrB_Vector_setElement_BOOL(q5, True, src))
+            ok(lib.GrB_Vector_assign_INT32(v5, q5, None, 1, lib.GrB_ALL, n, None), "stamp")
+            ok(lib.GrB_Vector_nvals(ctypes.byref(nv), v5), "read v between the stamp and the SpMV")
+            out["v_count"] = nv.value
+            r0 = stat(gb, "stat_bfs_root_push")
+            ok(lib.GrB_vxm(q5, v5, None, sr, q5, A._carg, lib.GrB_DESC_RSC), "level 1")
+            out["level1"] = bits(q5)[0]
+            q6, v6 = fresh(), fresh(lib.GrB_INT32)
+            ok(lib.GrB_Vector_setElement_BOOL(q6, True, src))
+            ok(lib.GrB_Vector_assign_INT32(v6, q6, None, 1, lib.GrB_ALL, n, None), "stamp")
+            ok(lib.GrB_vxm(q6, v6, None, sr, q6, A._carg, lib.GrB_DESC_RSC), "level 1 (root consumed)")
+            out["level1_consumed"] = bits(q6)[0]
+            out["v6"] = read_vec(lib, v6, n)[0][src]
+            out["root_pushes"] = stat(gb, "stat_bfs_root_push") - r0
+            for x in (q, q2, w, q3, m, q4, q5, v5, q6, v6):
+                lib.GrB_Vector_free(ctypes.byref(x))
+            results.append(out)
+        finally:
+            gb.set_knob("root_defer", 0)
+    on, off = results
+    assert on["tuples"] == off["tuples"] == ([src], [True])
+    assert on["vxm_other"] == off["vxm_other"] == succ
+    assert on["as_mask"] == off["as_mask"] == [src]
+    assert on["two"] == off["two"] == sorted({src, (src + 1) % n})
+    assert on["v_count"] == off["v_count"] == 1
+    expect = [j for j in succ if j != src]
+    assert on["level1"] == off["level1"] == expect
+    assert on["level1_consumed"] == off["level1_consumed"] == expect
+    assert on["v6"] == off["v6"] == 1
+    assert on["root_pushes"] >= 1 and off["root_pushes"] == 0
