@@ -38,7 +38,7 @@ namespace {
 constexpr int DT_BLOCK = 256;
 constexpr int DT_SMALL = 64;      // long side <= 64: k_dot_small, keys one per lane
 constexpr int DT_MID = 256;       // long side <= 256: k_dot_small, four keys per lane
-constexpr int DT_CAP = 8192;      // long side <= DT_CAP: k_dot_task (keys in LDS)
+constexpr int DT_CAP = 8191;      // long side <= DT_CAP: k_dot_task (keys in LDS, a 13-level Eytzinger tree)
 constexpr int DT_OVH = 64;        // per-entry cost added to the streamed length (task windows)
 constexpr int DT_OVH_MIN = 64;    // the least per-entry cost (knob dot_ovh): sizes the task's entry arrays
 constexpr int DT_WIN = 32768;     // task window: <= DT_WIN / ovh entries start in one
@@ -605,11 +605,22 @@ constexpr int DT_FLOG = 17;      // filter bits (log2)
 
 __device__ __forceinline__ uint32_t dt_hash(int32_t k) { return ((uint32_t)k * 0x9E3779B1u) >> (32 - DT_FLOG); }
 
-// LDS slot of X key i: a binary search over a power-of-two span probes keys m * 2^j - 1, which
-// all sit in one of the 64 banks while 2^j >= 64 (up to 64-way conflicts in the first seven
-// steps); skewing by i / 64 and i / 4096 spreads every step's probes over distinct banks
-constexpr int DT_KSLOTS = DT_CAP + DT_CAP / 64 + DT_CAP / 4096 + 1;
-__device__ __forceinline__ int dt_kp(int i) { return i + (i >> 6) + (i >> 12); }
+// X's keys sit in LDS in Eytzinger (breadth-first) order of a perfect search tree of h levels,
+// 1-based, padded with INT32_MAX (round 6): a lower-bound search is h steps of `j = 2 j + (keys[j] <
+// key)` -- one LDS read, a compare and a shift-add, against ~10 VALU per step for the round-5
+// sorted array with bank-skewed slots (index arithmetic, bounds test, select) -- and its first
+// levels are the same few words for every lane (broadcast reads).  Sorted index i of a tree of h
+// levels sits at node 2^d + ((i + 1) >> (t + 1)), t = ctz(i + 1), d = h - 1 - t; node k holds
+// sorted index ((2 (k - 2^d) + 1) << (h - 1 - d)) - 1, d = floor(log2 k).
+constexpr int DT_KSLOTS = 8192;  // nodes 1 .. 2^13 - 1
+__device__ __forceinline__ int dt_eytz(int i, int h) {
+    const int t = __builtin_ctz(i + 1);
+    return (1 << (h - 1 - t)) + ((i + 1) >> (t + 1));
+}
+__device__ __forceinline__ int dt_inorder(int k, int h) {
+    const int d = 31 - __builtin_clz(k);
+    return ((2 * (k - (1 << d)) + 1) << (h - 1 - d)) - 1;
+}
 
 // fold z into T's 4- or 8-byte output slot (pieces of one entry meet here; exact monoids)
 template <class SR, class Z>
@@ -668,11 +679,11 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
     const int64_t *__restrict__ eYS, const int32_t *__restrict__ eO, const int32_t *__restrict__ eB,
     const int64_t *__restrict__ eQ, Z *__restrict__ tval, uint8_t *__restrict__ tflag, int dbg,
     const uint16_t *__restrict__ ePc, int pcap, unsigned long long *__restrict__ tctr, int chunk) {
-    __shared__ int32_t keys[DT_KSLOTS];  // X's keys at dt_kp(i)
+    __shared__ int32_t keys[DT_KSLOTS];  // X's keys, Eytzinger order (dt_eytz)
     __shared__ uint32_t filt[1 << (DT_FLOG - 5)];
     __shared__ uint64_t estart[DT_SMAX / 64 + 1];     // bit f: an entry starts at flat element f
     __shared__ int32_t stage[DT_TB / 64][64 * DT_U];  // staged flat element | entry << 17
-    __shared__ int64_t e_ys[DT_MAXE];
+    __shared__ int64_t e_off[DT_MAXE];  // entry e's flat element f sits at Y position e_off[e] + f
     __shared__ int32_t e_pre[DT_MAXE + 1];
     __shared__ unsigned long long e_acc[DT_MAXE];
     __shared__ uint32_t e_fnd[DT_MAXE / 32];  // bit e: entry e found a match (the output slot and
@@ -718,7 +729,7 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
             b = eB[e0 + tid];
             ysv = eYS[e0 + tid];
         }
-        constexpr int XPT = DT_CAP / DT_TB;  // X keys per thread
+        constexpr int XPT = (DT_CAP + DT_TB - 1) / DT_TB;  // X keys per thread
         int32_t xk[XPT];
         if (!reuse) {
 #pragma unroll
@@ -729,7 +740,6 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
         for (int i = tid; i < DT_SMAX / 64 + 1; i += DT_TB) estart[i] = 0;
         for (int i = tid; i < DT_MAXE / 32; i += DT_TB) e_fnd[i] = 0;
         if (tid < ne) {
-            e_ys[tid] = ysv;
             unsigned long long iv = 0;
             __builtin_memcpy(&iv, &ident, sizeof(Z));
             e_acc[tid] = iv;
@@ -743,13 +753,15 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
         if (lane == 63) w_sum[wid] = inc;
         if (tid == 0) next_unit = 0;
         __syncthreads();  // filter and start bits cleared, wave sums visible
+        int ksteps = 0;  // tree levels: the least h with 2^h - 1 >= a
+        while ((1 << ksteps) - 1 < a) ksteps++;
         if (!reuse) {
 #pragma unroll
             for (int j = 0; j < XPT; j++) {
-                if (tid + j * DT_TB < a) {
-                    const int32_t k = xk[j];
-                    keys[dt_kp(tid + j * DT_TB)] = k;
-                    const uint32_t h = dt_hash(k);
+                const int i = tid + j * DT_TB;
+                if (i < (1 << ksteps) - 1) keys[dt_eytz(i, ksteps)] = i < a ? xk[j] : INT32_MAX;
+                if (i < a) {
+                    const uint32_t h = dt_hash(xk[j]);
                     atomicOr(&filt[h >> 5], 1u << (h & 31));
                 }
             }
@@ -763,12 +775,12 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
         if (tid < ne) {
             const int f = base + inc - b;
             e_pre[tid] = f;
+            e_off[tid] = ysv - f;
             if (b > 0) atomicOr((unsigned long long *)&estart[f >> 6], 1ULL << (f & 63));
         }
         if (tid == 0) e_pre[ne] = S;
         __syncthreads();
-        int ksteps = 0, esteps = 0;
-        while ((1 << ksteps) < a) ksteps++;
+        int esteps = 0;
         while ((1 << esteps) < ne) esteps++;
         const int NU = (S + DT_PIECE - 1) / DT_PIECE;
         // units (wave-uniform bookkeeping in scalar registers; no `continue` in the
@@ -812,7 +824,7 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
                 for (int u = 0; u < DT_U; u++) {
                     const int f = fb + u * 64 + lane;
                     const int eL = ee_o[u] < ne ? ee_o[u] : ne - 1;
-                    py[u] = f < fu1 ? e_ys[eL] + (f - e_pre[eL]) : 0;  // past the unit: a harmless load
+                    py[u] = f < fu1 ? e_off[eL] + f : 0;  // past the unit: a harmless load
                 }
 #pragma unroll
                 for (int u = 0; u < DT_U; u++) k_o[u] = s.yci[py[u]];
@@ -821,16 +833,15 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
             // loads the two values and folds into the lane's run (a lane's survivors come in
             // element order, hence in entry order)
             auto survivor = [&](bool act, int32_t kk, int f, int e) {
-                int l = 0;  // number of X keys < kk
-                for (int st = ksteps - 1; st >= 0; st--) {
-                    const int c = l + (1 << st);
-                    if (c <= a && keys[dt_kp(c - 1)] < kk) l = c;
-                }
-                if (act && !(dbg & 1) && l < a && keys[dt_kp(l)] == kk) {
+                int jn = 1;  // Eytzinger descent; the lower bound is the last node where it went left
+                for (int st = 0; st < ksteps; st++) jn = 2 * jn + (keys[jn] < kk ? 1 : 0);
+                const int kn = jn >> __builtin_ffs(~jn);  // 0: every key is < kk
+                if (act && !(dbg & 1) && kn && keys[kn] == kk) {
+                    const int l = dt_inorder(kn, ksteps);  // X's position of the key
                     X xv = X(), yv = X();
                     if (rv) {
                         xv = xvx[xs + l];
-                        yv = yvx[e_ys[e] + (f - e_pre[e])];
+                        yv = yvx[e_off[e] + f];
                     }
                     const Z z = dt_mult<SR, X, Z, SWAP>(sr, xv, yv, g, kk, eO[e0 + e]);
                     if (e != cur_e) {
@@ -867,7 +878,7 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
                         const bool act = r + lane < cnt;
                         const int w = act ? stg[r + lane] : 0;
                         const int f = w & 0x1ffff, e = w >> 17;
-                        const int64_t p = act ? e_ys[e] + (f - e_pre[e]) : 0;
+                        const int64_t p = act ? e_off[e] + f : 0;
                         survivor(act, act ? s.yci[p] : -1, f, e);
                     }
                     gb_wave_sync();  // the stage is rewritten by the next step
