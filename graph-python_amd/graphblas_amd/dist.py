@@ -410,9 +410,13 @@ class PeerFrontierExchange:
         lib = self.lib
         good = True
         try:
-            rows = [i - lo for i in range(lo, hi) if i % 7 == 3 or i == hi - 1]
-            for r in rows:
-                _ok(lib.GrB_Vector_setElement_BOOL(qloc, True, r), "setElement")
+            glob = np.arange(lo, hi, dtype=np.int64)
+            rows = np.ascontiguousarray(glob[(glob % 7 == 3) | (glob == hi - 1)] - lo, dtype=np.uint64)
+            vals = np.ones(rows.size, np.bool_)
+            _ok(lib.GrB_Vector_clear(qloc), "clear")
+            if rows.size:
+                _ok(lib.GrB_Vector_build_BOOL(qloc, ctypes.c_void_p(rows.ctypes.data), ctypes.c_void_p(vals.ctypes.data),
+                                              rows.size, None), "build")
             self.run(qloc, q)
             words = (n + 63) // 64
             got = torch.zeros(words, dtype=torch.int64, device="cuda")
