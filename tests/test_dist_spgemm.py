@@ -171,7 +171,7 @@ def _degree_sorted_fp64(G):
     return O.Csr.from_coo(rows, new[G.indices], G.values, nrows=G.nrows, ncols=G.ncols, dtype="FP64")
 
 
-def _balanced_worker(rank, world, port, scale, out_q):
+def _balanced_worker(rank, world, port, scale, out_q, mode=None):
     """bench.py config 5 at N > 1: equal-slot shards -> product-balanced bounds -> re-cut shards ->
     panel all-gather -> local product"""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -189,7 +189,7 @@ def _balanced_worker(rank, world, port, scale, out_q):
     rp = torch.from_numpy(G.indptr[lo:hi + 1] - p0)
     ci = torch.from_numpy(G.indices[p0:p1].astype(np.int32))
     vx = torch.from_numpy(G.values[p0:p1].copy())
-    g = gdist.RowPanelAllGather(dist, world, rank)
+    g = gdist.RowPanelAllGather(dist, world, rank, mode=mode)
     brp, bci, bvx, _ = g.run(rp, ci, vx)
     # the panels travel at their true sizes (no padding to the largest panel)
     true_rx = 0
@@ -206,10 +206,11 @@ def _balanced_worker(rank, world, port, scale, out_q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_product_balanced_bounds(world):
+@pytest.mark.parametrize("world,mode", [(2, None), (3, None), (3, "bcast")])
+def test_product_balanced_bounds(world, mode):
     """dist.product_balanced_bounds (bench.py config 5, N > 1): every rank derives the same row
-    ranges; the per-word products equal a direct count; each range carries at most total/world plus
+    ranges (mode "bcast": the panels move as the per-owner broadcasts RCCL uses; None: gloo's
+    send/recv pairs); the per-word products equal a direct count; each range carries at most total/world plus
     one word's products; on a hubs-first graph it evens out what equal slots leave on rank 0; and the
     stacked local products over the re-cut ranges are the oracle's C (bit-exact)"""
     scale = 9
@@ -225,7 +226,7 @@ def test_product_balanced_bounds(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_balanced_worker, args=(r, world, port, scale, q)) for r in range(world)]
+    procs = [ctx.Process(target=_balanced_worker, args=(r, world, port, scale, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
