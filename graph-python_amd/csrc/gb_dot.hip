@@ -28,6 +28,7 @@
 // Work is sum over mask entries of min(|A'(i,:)|, |B'^T(j,:)|) streamed keys
 // plus one LDS search each -- instead of a search in global memory per key.
 #include <algorithm>
+#include <climits>
 #include <cstdio>
 
 #include "gb_dispatch.cuh"
@@ -463,9 +464,33 @@ __device__ __forceinline__ void dt_lds_fold(const SR &sr, unsigned long long *sl
     }
 }
 
-// wave fold of (found, acc) into every lane (butterfly; exact monoids)
+extern "C" __device__ __attribute__((const)) long long __ockl_wfred_min_i64(long long);
+extern "C" __device__ __attribute__((const)) long long __ockl_wfred_add_i64(long long);
+
+// wave fold of (found, acc) into every lane (butterfly; exact monoids).  Callers reach it only when
+// some lane found a term.  Integer MIN and PLUS monoids use the device library's wavefront reduction
+// (DPP row operations, no LDS traffic) over the lanes' terms with the monoid's identity in the lanes
+// that found none (round 6): the butterfly's 6 steps x 3 ds_bpermute (a flag and two 32-bit halves)
+// were most of k_dot_small's LDS instructions
 template <class SR, class Z>
 __device__ __forceinline__ void dt_wave_fold(const SR &sr, bool &found, Z &acc) {
+    if constexpr (std::is_same<SR, gb_sr_min_plus<int64_t>>::value) {
+        acc = (Z)__ockl_wfred_min_i64(found ? (long long)acc : LLONG_MAX);
+        found = true;
+        return;
+    } else if constexpr (std::is_same<SR, gb_sr_min_plus<int32_t>>::value) {
+        acc = (Z)__ockl_wfred_min_i32(found ? (int)acc : INT_MAX);
+        found = true;
+        return;
+    } else if constexpr (std::is_same<SR, gb_sr_plus_times<int64_t>>::value) {
+        acc = (Z)__ockl_wfred_add_i64(found ? (long long)acc : 0LL);
+        found = true;
+        return;
+    } else if constexpr (std::is_same<SR, gb_sr_plus_times<int32_t>>::value) {
+        acc = (Z)__ockl_wfred_add_i32(found ? (int)acc : 0);
+        found = true;
+        return;
+    }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         const bool of = __shfl_xor((int)found, off, 64);
