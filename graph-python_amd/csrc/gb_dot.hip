@@ -515,9 +515,49 @@ __device__ __forceinline__ Z dt_mult(const SR &sr, X xv, X yv, int64_t g, int32_
 // 64 at a time (other index, Y bounds) and taken one after the other: lanes load
 // Y's keys 64 at a time (|Y| <= |X|) and find each among X's keys by shuffles --
 // 6 steps over the lanes' first keys, then the KPL keys of the lane found.
+// position of key yk among the wave's X keys (lane l holds X[l*KPL, l*KPL + KPL)), or -1
+template <int KPL>
+__device__ __forceinline__ int dt_small_find(const int32_t (&xk)[KPL], int32_t yk, bool act) {
+    int pos = -1;
+    if constexpr (KPL == 1) {
+        int lo = 0;
+#pragma unroll
+        for (int st = 32; st > 0; st >>= 1)
+            if (__shfl(xk[0], lo + st - 1, 64) < yk) lo += st;
+        // every lane takes part in the shuffle (a lane outside |Y| still serves its key)
+        const int32_t xl = __shfl(xk[0], lo, 64);
+        if (act && xl == yk) pos = lo;
+    } else {
+        int L = 0;  // last lane whose first key <= yk
+#pragma unroll
+        for (int st = 32; st > 0; st >>= 1) {
+            const int c = L + st;
+            const int32_t v = __shfl(xk[0], c < 64 ? c : 63, 64);
+            if (c < 64 && v <= yk) L = c;
+        }
+#pragma unroll
+        for (int j = 0; j < KPL; j++) {
+            const int32_t v = __shfl(xk[j], L, 64);
+            if (act && v == yk) pos = L * KPL + j;
+        }
+    }
+    return pos;
+}
+
+__device__ __forceinline__ int64_t dt_readlane64(int64_t v, int t) {
+    const int lo = __builtin_amdgcn_readlane((int)(v & 0xffffffff), t);
+    const int hi = __builtin_amdgcn_readlane((int)(v >> 32), t);
+    return (int64_t)(uint32_t)lo | ((int64_t)hi << 32);
+}
+
+// entries of a small group taken DT_SU at a time (round 6): their first 64 Y keys are loaded
+// together, then searched, then the hits' values loaded together -- one entry at a time left
+// every wave waiting on a key load, a dependent shuffle search and a value load per entry
+constexpr int DT_SU = 4;
+
 template <class SR, class X, class Z, bool SWAP, int KPL>
 __global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, dt_side s, dt_vals<X> xvx, dt_vals<X> yvx,
-                                                       Z *__restrict__ tval, uint8_t *__restrict__ tflag) {
+                                                       Z *__restrict__ tval, uint8_t *__restrict__ tflag, int seq) {
     const int lane = threadIdx.x & 63;
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const bool rv = SR::reads_values && xvx.v && yvx.v;
@@ -534,6 +574,85 @@ __global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, dt_side s, dt_val
         // X's values: read on a hit from the row just loaded (an L2 hit); round 4 held them in
         // registers beside the keys and shuffled KPL of them (two 32-bit shuffles each for 8-byte
         // values) for every 64 Y keys -- the kernel is bound by its shuffles, not by these loads
+        if (!seq) {
+            for (int64_t pb = p0; pb < p1; pb += 64) {
+                const int nb = __builtin_amdgcn_readfirstlane((int)std::min<int64_t>(64, p1 - pb));
+                int32_t o_l = 0;
+                int64_t ys_l = 0;
+                int b_l = 0;
+                if (lane < nb) {
+                    o_l = s.grp_oi[pb + lane];
+                    ys_l = s.yrp[o_l];
+                    b_l = (int)(s.yrp[o_l + 1] - ys_l);
+                }
+                unsigned long long todo = __ballot(lane < nb && b_l > 0 && dt_side_of<SWAP>(a, b_l));
+                while (todo) {
+                    int tt[DT_SU], bb[DT_SU];
+                    int64_t yss[DT_SU];
+#pragma unroll
+                    for (int u = 0; u < DT_SU; u++) {
+                        tt[u] = 0;
+                        bb[u] = 0;
+                        yss[u] = 0;
+                        if (todo) {
+                            const int t = __builtin_ctzll(todo);
+                            todo &= todo - 1;
+                            tt[u] = t;
+                            bb[u] = __builtin_amdgcn_readlane(b_l, t);
+                            yss[u] = dt_readlane64(ys_l, t);
+                        }
+                    }
+                    int32_t yk[DT_SU];
+#pragma unroll
+                    for (int u = 0; u < DT_SU; u++) yk[u] = lane < bb[u] ? s.yci[yss[u] + lane] : -1;
+                    int pos[DT_SU];
+#pragma unroll
+                    for (int u = 0; u < DT_SU; u++) pos[u] = dt_small_find<KPL>(xk, yk[u], lane < bb[u]);
+                    X xm[DT_SU], yv[DT_SU];
+#pragma unroll
+                    for (int u = 0; u < DT_SU; u++) {
+                        xm[u] = yv[u] = X();
+                        if (rv && pos[u] >= 0) {
+                            xm[u] = xvx[xs + pos[u]];
+                            yv[u] = yvx[yss[u] + lane];
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < DT_SU; u++) {
+                        if (bb[u] == 0) continue;  // wave-uniform
+                        const int32_t o = __builtin_amdgcn_readlane(o_l, tt[u]);
+                        bool found = pos[u] >= 0;
+                        Z acc = found ? dt_mult<SR, X, Z, SWAP>(sr, xm[u], yv[u], g, yk[u], o) : Z();
+                        // keys past the first 64 (|Y| <= 64 * KPL): one chunk at a time
+                        for (int f0 = 64; f0 < bb[u]; f0 += 64) {
+                            const bool act = f0 + lane < bb[u];
+                            const int32_t k2 = act ? s.yci[yss[u] + f0 + lane] : -1;
+                            const int p2 = dt_small_find<KPL>(xk, k2, act);
+                            if (p2 >= 0) {
+                                X x2 = X(), y2 = X();
+                                if (rv) {
+                                    x2 = xvx[xs + p2];
+                                    y2 = yvx[yss[u] + f0 + lane];
+                                }
+                                const Z z = dt_mult<SR, X, Z, SWAP>(sr, x2, y2, g, k2, o);
+                                acc = found ? sr.add(acc, z) : z;
+                                found = true;
+                            }
+                        }
+                        if (__ballot(found)) {
+                            dt_wave_fold(sr, found, acc);
+                            if (lane == 0) {
+                                const int64_t p = pb + tt[u];
+                                const int64_t q = s.perm ? s.perm[p] : p;
+                                tval[q] = acc;
+                                tflag[q] = 1;
+                            }
+                        }
+                    }
+                }
+            }
+            continue;
+        }
         for (int64_t pb = p0; pb < p1; pb += 64) {
             const int nb = __builtin_amdgcn_readfirstlane((int)std::min<int64_t>(64, p1 - pb));
             int32_t o_l = 0;
@@ -703,7 +822,7 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
     SR sr, int mon, dt_side s, dt_vals<X> xvx, dt_vals<X> yvx, int64_t ntask, const dt_task *__restrict__ tdesc, const int32_t *__restrict__ eG,
     const int64_t *__restrict__ eYS, const int32_t *__restrict__ eO, const int32_t *__restrict__ eB,
     const int64_t *__restrict__ eQ, Z *__restrict__ tval, uint8_t *__restrict__ tflag, int dbg,
-    const uint16_t *__restrict__ ePc, int pcap, unsigned long long *__restrict__ tctr, int chunk) {
+    const uint16_t *__restrict__ ePc, int pcap, unsigned long long *__restrict__ tctr, int chunk, int fratio) {
     __shared__ int32_t keys[DT_KSLOTS];  // X's keys, Eytzinger order (dt_eytz)
     __shared__ uint32_t filt[1 << (DT_FLOG - 5)];
     __shared__ uint64_t estart[DT_SMAX / 64 + 1];     // bit f: an entry starts at flat element f
@@ -729,6 +848,7 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
     __shared__ int64_t s_chunk;
     int64_t prev_g = -1;
     int prev_pc = -1;
+    bool fdirty = true;  // the filter holds bits (of the current X when a task reuses it)
     for (;;) {
     if (tid == 0) s_chunk = (int64_t)atomicAdd(tctr, (unsigned long long)chunk);
     __syncthreads();
@@ -737,6 +857,11 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
     if (c0 >= ntask) break;
     const int64_t c1 = c0 + chunk < ntask ? c0 + chunk : ntask;
     for (int64_t t = c0; t < c1; t++) {
+        // the thread index made opaque per task: otherwise the compiler hoists the per-thread
+        // Eytzinger slot arithmetic of every X key out of the task loop and spills it to scratch
+        // (38 VGPRs: reloaded from scratch in every task's setup)
+        int tv = tid;
+        asm volatile("" : "+v"(tv));
         const dt_task td = tdesc[t];  // one load (uniform)
         const int64_t e0 = td.e0;
         const int ne = __builtin_amdgcn_readfirstlane(td.ne);
@@ -747,27 +872,30 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
         prev_pc = piece;
         const int64_t xs = td.xs;
         const int a = __builtin_amdgcn_readfirstlane(td.a);
+        if (!reuse && tv == 0) atomicAdd(tctr + 1, 1ULL);  // X loads (stat dot_task_xloads)
         // the entries' and X's loads issued together, before any LDS work (one round trip)
         int b = 0;
         int64_t ysv = 0;
-        if (tid < ne) {
-            b = eB[e0 + tid];
-            ysv = eYS[e0 + tid];
+        if (tv < ne) {
+            b = eB[e0 + tv];
+            ysv = eYS[e0 + tv];
         }
         constexpr int XPT = (DT_CAP + DT_TB - 1) / DT_TB;  // X keys per thread
         int32_t xk[XPT];
         if (!reuse) {
 #pragma unroll
-            for (int j = 0; j < XPT; j++) xk[j] = tid + j * DT_TB < a ? s.xci[xs + tid + j * DT_TB] : 0;
+            for (int j = 0; j < XPT; j++) xk[j] = tv + j * DT_TB < a ? s.xci[xs + tv + j * DT_TB] : 0;
         }
-        if (!reuse)
-            for (int i = tid; i < (1 << (DT_FLOG - 5)); i += DT_TB) filt[i] = 0;
-        for (int i = tid; i < DT_SMAX / 64 + 1; i += DT_TB) estart[i] = 0;
-        for (int i = tid; i < DT_MAXE / 32; i += DT_TB) e_fnd[i] = 0;
-        if (tid < ne) {
+        if (!reuse && fdirty) {  // a filter of another X: cleared (the first task: LDS garbage)
+            for (int i = tv; i < (1 << (DT_FLOG - 5)); i += DT_TB) filt[i] = 0;
+            fdirty = false;
+        }
+        for (int i = tv; i < DT_SMAX / 64 + 1; i += DT_TB) estart[i] = 0;
+        for (int i = tv; i < DT_MAXE / 32; i += DT_TB) e_fnd[i] = 0;
+        if (tv < ne) {
             unsigned long long iv = 0;
             __builtin_memcpy(&iv, &ident, sizeof(Z));
-            e_acc[tid] = iv;
+            e_acc[tv] = iv;
         }
         int inc = b;
 #pragma unroll
@@ -776,34 +904,40 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
             if (lane >= off) inc += y;
         }
         if (lane == 63) w_sum[wid] = inc;
-        if (tid == 0) next_unit = 0;
+        if (tv == 0) next_unit = 0;
         __syncthreads();  // filter and start bits cleared, wave sums visible
         int ksteps = 0;  // tree levels: the least h with 2^h - 1 >= a
         while ((1 << ksteps) - 1 < a) ksteps++;
-        if (!reuse) {
-#pragma unroll
-            for (int j = 0; j < XPT; j++) {
-                const int i = tid + j * DT_TB;
-                if (i < (1 << ksteps) - 1) keys[dt_eytz(i, ksteps)] = i < a ? xk[j] : INT32_MAX;
-                if (i < a) {
-                    const uint32_t h = dt_hash(xk[j]);
-                    atomicOr(&filt[h >> 5], 1u << (h & 31));
-                }
-            }
-        }
         int base = 0, S = 0;
         for (int w = 0; w < DT_TB / 64; w++) {
             if (w < wid) base += w_sum[w];
             S += w_sum[w];
         }
         S = __builtin_amdgcn_readfirstlane(S);
-        if (tid < ne) {
+        // the hashed filter pays when the task streams enough keys past it (round 6, knob
+        // dot_filt_ratio: built only when S >= ratio * |X|; 0 = always); kept across tasks of one X
+        const bool usef = fratio <= 0 || S >= fratio * a;
+        const bool fbuild = usef && !fdirty;
+        if (!reuse || fbuild) {
+#pragma unroll
+            for (int j = 0; j < XPT; j++) {
+                const int i = tv + j * DT_TB;
+                if (!reuse && i < (1 << ksteps) - 1) keys[dt_eytz(i, ksteps)] = i < a ? xk[j] : INT32_MAX;
+                if (fbuild && i < a) {
+                    const int32_t kx = reuse ? keys[dt_eytz(i, ksteps)] : xk[j];
+                    const uint32_t h = dt_hash(kx);
+                    atomicOr(&filt[h >> 5], 1u << (h & 31));
+                }
+            }
+        }
+        fdirty = fdirty || fbuild;
+        if (tv < ne) {
             const int f = base + inc - b;
-            e_pre[tid] = f;
-            e_off[tid] = ysv - f;
+            e_pre[tv] = f;
+            e_off[tv] = ysv - f;
             if (b > 0) atomicOr((unsigned long long *)&estart[f >> 6], 1ULL << (f & 63));
         }
-        if (tid == 0) e_pre[ne] = S;
+        if (tv == 0) e_pre[ne] = S;
         __syncthreads();
         int esteps = 0;
         while ((1 << esteps) < ne) esteps++;
@@ -893,7 +1027,7 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
                     for (int u = 0; u < DT_U; u++) {
                         const int f = f0 + u * 64 + lane;
                         const uint32_t h = dt_hash((dbg & 4) ? f : k[u]);
-                        const bool c = !(dbg & 2) && f < fu1 && ((filt[h >> 5] >> (h & 31)) & 1u);
+                        const bool c = !(dbg & 2) && f < fu1 && (!usef || ((filt[h >> 5] >> (h & 31)) & 1u));
                         const unsigned long long m = __ballot(c);
                         if (c) stg[cnt + __popcll(m & ltmask)] = f | (ee[u] << 17);
                         cnt += __popcll(m);
@@ -926,7 +1060,7 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
 #pragma unroll
                     for (int u = 0; u < DT_U; u++) hh[u] = dt_hash((dbg & 4) ? f0 + u * 64 + lane : k[u]);
 #pragma unroll
-                    for (int u = 0; u < DT_U; u++) fw[u] = filt[hh[u] >> 5];
+                    for (int u = 0; u < DT_U; u++) fw[u] = usef ? filt[hh[u] >> 5] : ~0u;
 #pragma unroll
                     for (int u = 0; u < DT_U; u++) {
                         const int f = f0 + u * 64 + lane;
@@ -972,10 +1106,10 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
             unit = __builtin_amdgcn_readlane(nxt, 0);
         }
         __syncthreads();
-        if (tid < ne && ((e_fnd[tid >> 5] >> (tid & 31)) & 1u)) {
-            const int64_t q = eQ[e0 + tid];
+        if (tv < ne && ((e_fnd[tv >> 5] >> (tv & 31)) & 1u)) {
+            const int64_t q = eQ[e0 + tv];
             Z v;
-            const unsigned long long raw = e_acc[tid];
+            const unsigned long long raw = e_acc[tv];
             __builtin_memcpy(&v, &raw, sizeof(Z));
             if (piece >= 0) dt_global_fold(sr, ANY, &tval[q], v);
             else tval[q] = v;
@@ -1053,12 +1187,13 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
             const dt_vals<X> xv = SWAP ? vb : va, yv = SWAP ? va : vb;
             if (!SWAP && SRT::reads_values && (va.nk || vb.nk)) gb_stat_add("dot_narrow_calls", 1);
             const unsigned gw = dt_grid(sd.ng * 64, DT_BLOCK, 1 << 15);
+            const int sseq = gb_knob("dot_small_seq") == 1;  // 1: one entry at a time (the round-5 loop, A/B)
             hipLaunchKernelGGL((k_dot_small<SRT, X, Z, SWAP, 1>), dim3(gw), dim3(DT_BLOCK), 0, gb_stream(), srf, sd,
-                               xv, yv, (Z *)tval, tflag);
+                               xv, yv, (Z *)tval, tflag, sseq);
             const int64_t skip = gb_knob("dot_skip");  // diagnostics: 1 skips the mid kernel, 2 the task kernel
             if (!(skip & 1))
                 hipLaunchKernelGGL((k_dot_small<SRT, X, Z, SWAP, DT_MID / 64>), dim3(gw), dim3(DT_BLOCK), 0,
-                                   gb_stream(), srf, sd, xv, yv, (Z *)tval, tflag);
+                                   gb_stream(), srf, sd, xv, yv, (Z *)tval, tflag, sseq);
             // lists longer than the cap run as pieces of cap keys (4- and 8-byte results:
             // the pieces of an entry fold into its output slot with atomics)
             const bool pieces = (sizeof(Z) == 4 || sizeof(Z) == 8) && gb_knob("dot_pieces") != 1;
@@ -1136,8 +1271,8 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
                 GB_LAUNCH_CHECK();
                 // persistent workgroups (two per CU) taking chunks of consecutive tasks
                 const unsigned gt = (unsigned)std::min<int64_t>(nt, 1024);
-                unsigned long long *tctr = ts.get<unsigned long long>(1);
-                gb_memset(tctr, 0, sizeof(unsigned long long));
+                unsigned long long *tctr = ts.get<unsigned long long>(2);  // [0] chunk counter, [1] X loads
+                gb_memset(tctr, 0, 2 * sizeof(unsigned long long));
                 // tools/spgemm_probe.py (R-MAT, one box): chunk 1/4/8/16/32 -> s20 24.7/24.1/25.3/27.7/33.0 ms,
                 // s22 (1/8/32) 128.6/121.5/136.3 ms
                 int64_t chunk = gb_knob("dot_chunk");
@@ -1145,8 +1280,13 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
                 if (!(skip & 2))
                     hipLaunchKernelGGL((k_dot_task<SRT, X, Z, SWAP>), dim3(gt), dim3(DT_TB), 0, gb_stream(), srf,
                                        info.mon, sd, xv, yv, nt, tdesc, eG, eYS, eO, eB, eQ, (Z *)tval,
-                                       tflag, (int)gb_knob("dot_dbg"), ePc, cap, tctr, (int)chunk);
+                                       tflag, (int)gb_knob("dot_dbg"), ePc, cap, tctr, (int)chunk,
+                                       (int)gb_knob("dot_filt_ratio"));
                 GB_LAUNCH_CHECK();
+                if (gb_knob("dot_stats") == 1) {  // diagnostics: a host read per launch
+                    gb_stat_add(ePc ? "dot_piece_tasks" : "dot_tasks", nt);
+                    gb_stat_add("dot_task_xloads", gb_read_i64((const int64_t *)tctr + 1));
+                }
             };
             gb_exclusive_scan_u8(tf, pos, nm);
             const int64_t ne = gb_read_i64(pos + nm);
