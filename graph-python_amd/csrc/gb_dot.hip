@@ -826,7 +826,9 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
     __shared__ int32_t keys[DT_KSLOTS];  // X's keys, Eytzinger order (dt_eytz)
     __shared__ uint32_t filt[1 << (DT_FLOG - 5)];
     __shared__ uint64_t estart[DT_SMAX / 64 + 1];     // bit f: an entry starts at flat element f
-    __shared__ int32_t stage[DT_TB / 64][64 * DT_U];  // staged flat element | entry << 17
+    // X's values when they are one-byte narrow copies (round 6): a hit reads its X value from LDS
+    // instead of global memory (the round-4 staged-survivor diagnostics path held this LDS)
+    __shared__ uint8_t xv8[DT_KSLOTS];
     __shared__ int64_t e_off[DT_MAXE];  // entry e's flat element f sits at Y position e_off[e] + f
     __shared__ int32_t e_pre[DT_MAXE + 1];
     __shared__ unsigned long long e_acc[DT_MAXE];
@@ -836,12 +838,15 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
     __shared__ int next_unit;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const bool rv = SR::reads_values && xvx.v && yvx.v;
+    // one-byte narrow X values go to LDS with the keys (knob dot_xlds = 1: off, A/B)
+    bool xl8 = false;
+    if constexpr (std::is_integral<X>::value && !std::is_same<X, bool>::value && sizeof(X) > 1)
+        xl8 = rv && !xvx.iso && xvx.nv && (xvx.nk == 1 || xvx.nk == -1) && !(dbg & 4096);
     // ANY (any_pair, or LOR over pair's 1s): the entry's value is any term -- store it;
     // every other monoid folds into its identity
     const bool ANY = std::is_same<SR, gb_sr_any_pair<Z>>::value || mon == GBAMD_MON_ANY;
     const Z ident = ANY ? Z() : gb_monoid_identity<Z>(mon);
     const unsigned long long ltmask = (1ULL << lane) - 1;
-    int32_t *stg = stage[wid];
     // tasks are handed out in chunks of `chunk` consecutive tasks from a grid-wide counter
     // (dynamic: the workgroups stay balanced); consecutive tasks of one group share X(g,:),
     // whose keys and filter then stay in LDS
@@ -885,6 +890,12 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
         if (!reuse) {
 #pragma unroll
             for (int j = 0; j < XPT; j++) xk[j] = tv + j * DT_TB < a ? s.xci[xs + tv + j * DT_TB] : 0;
+            if (xl8) {
+                const uint8_t *nv = (const uint8_t *)xvx.nv;
+#pragma unroll
+                for (int j = 0; j < XPT; j++)
+                    if (tv + j * DT_TB < a) xv8[tv + j * DT_TB] = nv[xs + tv + j * DT_TB];
+            }
         }
         if (!reuse && fdirty) {  // a filter of another X: cleared (the first task: LDS garbage)
             for (int i = tv; i < (1 << (DT_FLOG - 5)); i += DT_TB) filt[i] = 0;
@@ -999,7 +1010,8 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
                     const int l = dt_inorder(kn, ksteps);  // X's position of the key
                     X xv = X(), yv = X();
                     if (rv) {
-                        xv = xvx[xs + l];
+                        if (xl8) xv = xvx.nk == 1 ? (X)xv8[l] : (X)(int8_t)xv8[l];
+                        else xv = xvx[xs + l];
                         yv = yvx[e_off[e] + f];
                     }
                     const Z z = dt_mult<SR, X, Z, SWAP>(sr, xv, yv, g, kk, eO[e0 + e]);
@@ -1015,34 +1027,7 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
                     found = true;
                 }
             };
-            if (dbg & 256) {
-                // diagnostics (A/B): round 4's survivors staged in LDS as (element, entry) and their
-                // keys loaded again from global memory before the search
-                for (int f0 = fu0; f0 < ((dbg & 8) ? fu0 : fu1); f0 += 64 * DT_U) {
-                    int cnt = 0;
-                    int32_t k[DT_U];
-                    int ee[DT_U];
-                    issue(f0, ee, k);
-#pragma unroll
-                    for (int u = 0; u < DT_U; u++) {
-                        const int f = f0 + u * 64 + lane;
-                        const uint32_t h = dt_hash((dbg & 4) ? f : k[u]);
-                        const bool c = !(dbg & 2) && f < fu1 && (!usef || ((filt[h >> 5] >> (h & 31)) & 1u));
-                        const unsigned long long m = __ballot(c);
-                        if (c) stg[cnt + __popcll(m & ltmask)] = f | (ee[u] << 17);
-                        cnt += __popcll(m);
-                    }
-                    gb_wave_sync();
-                    for (int r = 0; r < cnt; r += 64) {
-                        const bool act = r + lane < cnt;
-                        const int w = act ? stg[r + lane] : 0;
-                        const int f = w & 0x1ffff, e = w >> 17;
-                        const int64_t p = act ? e_off[e] + f : 0;
-                        survivor(act, act ? s.yci[p] : -1, f, e);
-                    }
-                    gb_wave_sync();  // the stage is rewritten by the next step
-                }
-            } else {
+            {
                 // Survivors are compacted in registers: each window's passing keys and their
                 // (element | entry << 17) words are forward-permuted (ds_permute, no LDS storage)
                 // into lanes [pc, pc + n) of a 64-lane batch -- the other lanes' values go to the
@@ -1280,7 +1265,8 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
                 if (!(skip & 2))
                     hipLaunchKernelGGL((k_dot_task<SRT, X, Z, SWAP>), dim3(gt), dim3(DT_TB), 0, gb_stream(), srf,
                                        info.mon, sd, xv, yv, nt, tdesc, eG, eYS, eO, eB, eQ, (Z *)tval,
-                                       tflag, (int)gb_knob("dot_dbg"), ePc, cap, tctr, (int)chunk,
+                                       tflag, (int)gb_knob("dot_dbg") | (gb_knob("dot_xlds") == 1 ? 4096 : 0), ePc,
+                                       cap, tctr, (int)chunk,
                                        (int)gb_knob("dot_filt_ratio"));
                 GB_LAUNCH_CHECK();
                 if (gb_knob("dot_stats") == 1) {  // diagnostics: a host read per launch
