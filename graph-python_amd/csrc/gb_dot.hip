@@ -842,6 +842,11 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
     bool xl8 = false;
     if constexpr (std::is_integral<X>::value && !std::is_same<X, bool>::value && sizeof(X) > 1)
         xl8 = rv && !xvx.iso && xvx.nv && (xvx.nk == 1 || xvx.nk == -1) && !(dbg & 4096);
+    // one-byte narrow Y values streamed with the keys, packed in the key's top byte when the keys
+    // are below 2^24 (knob dot_ypack = 1: off), so a hit loads nothing from global memory
+    bool yp8 = false;
+    if constexpr (std::is_integral<X>::value && !std::is_same<X, bool>::value && sizeof(X) > 1)
+        yp8 = rv && !yvx.iso && yvx.nv && (yvx.nk == 1 || yvx.nk == -1) && (dbg & 8192);
     // ANY (any_pair, or LOR over pair's 1s): the entry's value is any term -- store it;
     // every other monoid folds into its identity
     const bool ANY = std::is_same<SR, gb_sr_any_pair<Z>>::value || mon == GBAMD_MON_ANY;
@@ -998,11 +1003,20 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
                 }
 #pragma unroll
                 for (int u = 0; u < DT_U; u++) k_o[u] = s.yci[py[u]];
+                if (yp8) {  // one-byte Y values ride in the key's top byte (keys < 2^24)
+                    const uint8_t *nv = (const uint8_t *)yvx.nv;
+                    uint32_t v8[DT_U];
+#pragma unroll
+                    for (int u = 0; u < DT_U; u++) v8[u] = nv[py[u]];
+#pragma unroll
+                    for (int u = 0; u < DT_U; u++) k_o[u] = (int32_t)((uint32_t)k_o[u] | (v8[u] << 24));
+                }
             };
             // one surviving element (its key passed the filter): binary search in X's keys; a hit
             // loads the two values and folds into the lane's run (a lane's survivors come in
             // element order, hence in entry order)
-            auto survivor = [&](bool act, int32_t kk, int f, int e) {
+            auto survivor = [&](bool act, int32_t kp, int f, int e) {
+                const int32_t kk = yp8 ? (kp & 0xffffff) : kp;
                 int jn = 1;  // Eytzinger descent; the lower bound is the last node where it went left
                 for (int st = 0; st < ksteps; st++) jn = 2 * jn + (keys[jn] < kk ? 1 : 0);
                 const int kn = jn >> __builtin_ffs(~jn);  // 0: every key is < kk
@@ -1012,7 +1026,8 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
                     if (rv) {
                         if (xl8) xv = xvx.nk == 1 ? (X)xv8[l] : (X)(int8_t)xv8[l];
                         else xv = xvx[xs + l];
-                        yv = yvx[e_off[e] + f];
+                        if (yp8) yv = yvx.nk == 1 ? (X)((uint32_t)kp >> 24) : (X)(int8_t)((uint32_t)kp >> 24);
+                        else yv = yvx[e_off[e] + f];
                     }
                     const Z z = dt_mult<SR, X, Z, SWAP>(sr, xv, yv, g, kk, eO[e0 + e]);
                     if (e != cur_e) {
@@ -1043,7 +1058,8 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
                     issue(f0, ee, k);
                     uint32_t hh[DT_U], fw[DT_U];
 #pragma unroll
-                    for (int u = 0; u < DT_U; u++) hh[u] = dt_hash((dbg & 4) ? f0 + u * 64 + lane : k[u]);
+                    for (int u = 0; u < DT_U; u++)
+                        hh[u] = dt_hash((dbg & 4) ? f0 + u * 64 + lane : (yp8 ? (k[u] & 0xffffff) : k[u]));
 #pragma unroll
                     for (int u = 0; u < DT_U; u++) fw[u] = usef ? filt[hh[u] >> 5] : ~0u;
 #pragma unroll
@@ -1116,6 +1132,7 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
     const int64_t nm = mask.nvals;
     *huge = nullptr;
     if (nm == 0) return 0;
+    const int64_t nkey = std::max(A.ncols, BT.ncols);  // the inner dimension: the lists' keys are below it
     gb_scratch s;
     // the mask's CSC with each entry's CSR position: cached on the mask matrix, or built
     const int64_t *mtrp, *mperm;
@@ -1265,7 +1282,10 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
                 if (!(skip & 2))
                     hipLaunchKernelGGL((k_dot_task<SRT, X, Z, SWAP>), dim3(gt), dim3(DT_TB), 0, gb_stream(), srf,
                                        info.mon, sd, xv, yv, nt, tdesc, eG, eYS, eO, eB, eQ, (Z *)tval,
-                                       tflag, (int)gb_knob("dot_dbg") | (gb_knob("dot_xlds") == 1 ? 4096 : 0), ePc,
+                                       tflag,
+                                       (int)gb_knob("dot_dbg") | (gb_knob("dot_xlds") == 1 ? 4096 : 0) |
+                                           ((gb_knob("dot_ypack") != 1 && nkey <= (1LL << 24)) ? 8192 : 0),
+                                       ePc,
                                        cap, tctr, (int)chunk,
                                        (int)gb_knob("dot_filt_ratio"));
                 GB_LAUNCH_CHECK();
