@@ -882,7 +882,9 @@ __global__ __launch_bounds__(DT_TB, 8) void k_dot_task(
         prev_pc = piece;
         const int64_t xs = td.xs;
         const int a = __builtin_amdgcn_readfirstlane(td.a);
-        if (!reuse && tv == 0) atomicAdd(tctr + 1, 1ULL);  // X loads (stat dot_task_xloads)
+        // X loads (stat dot_task_xloads), counted only under the statistics knob and a cache line
+        // away from the chunk counter the workgroups claim tasks from
+        if ((dbg & 1024) && !reuse && tv == 0) atomicAdd(tctr + 16, 1ULL);
         // the entries' and X's loads issued together, before any LDS work (one round trip)
         int b = 0;
         int64_t ysv = 0;
@@ -1273,8 +1275,9 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
                 GB_LAUNCH_CHECK();
                 // persistent workgroups (two per CU) taking chunks of consecutive tasks
                 const unsigned gt = (unsigned)std::min<int64_t>(nt, 1024);
-                unsigned long long *tctr = ts.get<unsigned long long>(2);  // [0] chunk counter, [1] X loads
-                gb_memset(tctr, 0, 2 * sizeof(unsigned long long));
+                unsigned long long *tctr = ts.get<unsigned long long>(17);  // [0] chunk counter, [16] X loads
+                gb_memset(tctr, 0, 17 * sizeof(unsigned long long));
+                const bool dstat = gb_knob("dot_stats") == 1;
                 // tools/spgemm_probe.py (R-MAT, one box): chunk 1/4/8/16/32 -> s20 24.7/24.1/25.3/27.7/33.0 ms,
                 // s22 (1/8/32) 128.6/121.5/136.3 ms
                 int64_t chunk = gb_knob("dot_chunk");
@@ -1283,15 +1286,15 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
                     hipLaunchKernelGGL((k_dot_task<SRT, X, Z, SWAP>), dim3(gt), dim3(DT_TB), 0, gb_stream(), srf,
                                        info.mon, sd, xv, yv, nt, tdesc, eG, eYS, eO, eB, eQ, (Z *)tval,
                                        tflag,
-                                       (int)gb_knob("dot_dbg") | (gb_knob("dot_xlds") == 1 ? 4096 : 0) |
+                                       (int)gb_knob("dot_dbg") | (gb_knob("dot_xlds") == 1 ? 4096 : 0) | (dstat ? 1024 : 0) |
                                            ((gb_knob("dot_ypack") != 1 && nkey <= (1LL << 24)) ? 8192 : 0),
                                        ePc,
                                        cap, tctr, (int)chunk,
                                        (int)gb_knob("dot_filt_ratio"));
                 GB_LAUNCH_CHECK();
-                if (gb_knob("dot_stats") == 1) {  // diagnostics: a host read per launch
+                if (dstat) {  // diagnostics: a host read per launch
                     gb_stat_add(ePc ? "dot_piece_tasks" : "dot_tasks", nt);
-                    gb_stat_add("dot_task_xloads", gb_read_i64((const int64_t *)tctr + 1));
+                    gb_stat_add("dot_task_xloads", gb_read_i64((const int64_t *)tctr + 16));
                 }
             };
             gb_exclusive_scan_u8(tf, pos, nm);
