@@ -464,6 +464,18 @@ __device__ __forceinline__ void dt_lds_fold(const SR &sr, unsigned long long *sl
     }
 }
 
+// fold z into an LDS slot; ANY stores (any term is the result)
+template <class SR, class Z>
+__device__ __forceinline__ void dt_slot_fold(const SR &sr, bool any_store, unsigned long long *slot, Z z) {
+    if (any_store) {
+        unsigned long long v = 0;
+        __builtin_memcpy(&v, &z, sizeof(Z));
+        *slot = v;
+    } else {
+        dt_lds_fold(sr, slot, z);
+    }
+}
+
 extern "C" __device__ __attribute__((const)) long long __ockl_wfred_min_i64(long long);
 extern "C" __device__ __attribute__((const)) long long __ockl_wfred_add_i64(long long);
 
@@ -555,13 +567,28 @@ __device__ __forceinline__ int64_t dt_readlane64(int64_t v, int t) {
 // every wave waiting on a key load, a dependent shuffle search and a value load per entry
 constexpr int DT_SU = 4;
 
+// Flat entries (round 6, the default): a batch's entries' Y lists are one flat run of keys, 64 per
+// lane-step and DT_FU steps at a time -- a lane finds its element's entry by a shuffle search over
+// the entries' prefix -- so short Y lists no longer leave most of a wave idle; a hit (a few % of
+// the keys in these classes) folds into its entry's LDS slot by an atomic, so there is no
+// segmented scan.  Used with four keys per lane; seq 1: one entry at a time (A/B).
+constexpr int DT_FU = 4;
+
 template <class SR, class X, class Z, bool SWAP, int KPL>
-__global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, dt_side s, dt_vals<X> xvx, dt_vals<X> yvx,
+__global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, int mon, dt_side s, dt_vals<X> xvx, dt_vals<X> yvx,
                                                        Z *__restrict__ tval, uint8_t *__restrict__ tflag, int seq) {
     const int lane = threadIdx.x & 63;
     const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const bool rv = SR::reads_values && xvx.v && yvx.v;
     constexpr int AMIN = KPL == 1 ? 1 : DT_SMALL + 1;
+    __shared__ unsigned long long f_slot[DT_BLOCK / 64][64];
+    __shared__ unsigned long long f_found[DT_BLOCK / 64];
+    unsigned long long *fslot = f_slot[threadIdx.x >> 6];
+    unsigned long long *ffound = &f_found[threadIdx.x >> 6];
+    const bool ANY = std::is_same<SR, gb_sr_any_pair<Z>>::value || mon == GBAMD_MON_ANY;
+    const Z ident = ANY ? Z() : gb_monoid_identity<Z>(mon);
+    unsigned long long identb = 0;
+    __builtin_memcpy(&identb, &ident, sizeof(Z));
     for (int64_t g = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; g < s.ng; g += nw) {
         const int64_t xs = s.xrp[g];
         const int a = __builtin_amdgcn_readfirstlane((int)(s.xrp[g + 1] - xs));
@@ -574,7 +601,80 @@ __global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, dt_side s, dt_val
         // X's values: read on a hit from the row just loaded (an L2 hit); round 4 held them in
         // registers beside the keys and shuffled KPL of them (two 32-bit shuffles each for 8-byte
         // values) for every 64 Y keys -- the kernel is bound by its shuffles, not by these loads
-        if (!seq) {
+        // four keys per lane (X of 65..256 keys): flat entries; one key per lane: DT_SU entries at a
+        // time (measured: the flat form wins with four keys per lane and loses with one)
+        if (KPL > 1 && !seq) {
+            for (int64_t pb = p0; pb < p1; pb += 64) {
+                const int nb = __builtin_amdgcn_readfirstlane((int)std::min<int64_t>(64, p1 - pb));
+                int32_t o_l = 0;
+                int64_t ys_l = 0;
+                int b_l = 0;
+                if (lane < nb) {
+                    o_l = s.grp_oi[pb + lane];
+                    ys_l = s.yrp[o_l];
+                    b_l = (int)(s.yrp[o_l + 1] - ys_l);
+                }
+                const int bl = (lane < nb && b_l > 0 && dt_side_of<SWAP>(a, b_l)) ? b_l : 0;
+                int inc = bl;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const int y = __shfl_up(inc, off, 64);
+                    if (lane >= off) inc += y;
+                }
+                const int T = __builtin_amdgcn_readlane(inc, 63);
+                if (T == 0) continue;  // wave-uniform
+                const int64_t yoff_l = ys_l - (inc - bl);  // entry e's flat element f sits at Y position yoff_e + f
+                fslot[lane] = identb;
+                if (lane == 0) *ffound = 0ULL;
+                gb_wave_sync();
+                for (int f0 = 0; f0 < T; f0 += 64 * DT_FU) {
+                    int ee[DT_FU];
+                    int64_t py[DT_FU];
+                    int32_t yk[DT_FU];
+#pragma unroll
+                    for (int u = 0; u < DT_FU; u++) {
+                        const int f = f0 + u * 64 + lane;
+                        int lo = 0;  // the first entry whose inclusive prefix exceeds f
+#pragma unroll
+                        for (int st = 32; st > 0; st >>= 1)
+                            if (__shfl(inc, lo + st - 1, 64) <= f) lo += st;
+                        ee[u] = lo;
+                        py[u] = gb_shfl(yoff_l, lo < 64 ? lo : 63) + f;
+                        yk[u] = f < T ? s.yci[py[u]] : -1;
+                    }
+                    int pos[DT_FU];
+#pragma unroll
+                    for (int u = 0; u < DT_FU; u++) pos[u] = dt_small_find<KPL>(xk, yk[u], f0 + u * 64 + lane < T);
+#pragma unroll
+                    for (int u = 0; u < DT_FU; u++) {
+                        const int32_t o = __shfl(o_l, ee[u] < 64 ? ee[u] : 63, 64);  // every lane shuffles
+                        if (pos[u] >= 0) {
+                            X xm = X(), yv = X();
+                            if (rv) {
+                                xm = xvx[xs + pos[u]];
+                                yv = yvx[py[u]];
+                            }
+                            const Z z = dt_mult<SR, X, Z, SWAP>(sr, xm, yv, g, yk[u], o);
+                            dt_slot_fold(sr, ANY, &fslot[ee[u]], z);
+                            atomicOr(ffound, 1ULL << ee[u]);
+                        }
+                    }
+                }
+                gb_wave_sync();
+                if (lane < nb && ((*ffound >> lane) & 1ULL)) {
+                    const int64_t p = pb + lane;
+                    const int64_t q = s.perm ? s.perm[p] : p;
+                    Z v;
+                    const unsigned long long raw = fslot[lane];
+                    __builtin_memcpy(&v, &raw, sizeof(Z));
+                    tval[q] = v;
+                    tflag[q] = 1;
+                }
+                gb_wave_sync();  // the slots are rewritten by the next batch
+            }
+            continue;
+        }
+        if (KPL == 1 && !seq) {
             for (int64_t pb = p0; pb < p1; pb += 64) {
                 const int nb = __builtin_amdgcn_readfirstlane((int)std::min<int64_t>(64, p1 - pb));
                 int32_t o_l = 0;
@@ -804,16 +904,6 @@ __device__ __forceinline__ void dt_global_fold(const SR &sr, bool any_store, Z *
     }
 }
 
-template <class SR, class Z>
-__device__ __forceinline__ void dt_slot_fold(const SR &sr, bool any_store, unsigned long long *slot, Z z) {
-    if (any_store) {
-        unsigned long long v = 0;
-        __builtin_memcpy(&v, &z, sizeof(Z));
-        *slot = v;
-    } else {
-        dt_lds_fold(sr, slot, z);
-    }
-}
 
 template <class SR, class X, class Z, bool SWAP>
 // 8 waves per SIMD: two workgroups per CU (round 3: one workgroup of 149.6 KB LDS and 78 VGPRs
@@ -1191,13 +1281,14 @@ int64_t gb_dot_two_sided(const gb_csr_view &A, const gb_csr_view &BT, gb_mmask &
             const dt_vals<X> xv = SWAP ? vb : va, yv = SWAP ? va : vb;
             if (!SWAP && SRT::reads_values && (va.nk || vb.nk)) gb_stat_add("dot_narrow_calls", 1);
             const unsigned gw = dt_grid(sd.ng * 64, DT_BLOCK, 1 << 15);
-            const int sseq = gb_knob("dot_small_seq") == 1;  // 1: one entry at a time (the round-5 loop, A/B)
-            hipLaunchKernelGGL((k_dot_small<SRT, X, Z, SWAP, 1>), dim3(gw), dim3(DT_BLOCK), 0, gb_stream(), srf, sd,
-                               xv, yv, (Z *)tval, tflag, sseq);
+            // 1: one entry at a time (the round-5 loop, A/B)
+            const int sseq = gb_knob("dot_small_seq") == 1 ? 1 : 0;
+            hipLaunchKernelGGL((k_dot_small<SRT, X, Z, SWAP, 1>), dim3(gw), dim3(DT_BLOCK), 0, gb_stream(), srf,
+                               info.mon, sd, xv, yv, (Z *)tval, tflag, sseq);
             const int64_t skip = gb_knob("dot_skip");  // diagnostics: 1 skips the mid kernel, 2 the task kernel
             if (!(skip & 1))
                 hipLaunchKernelGGL((k_dot_small<SRT, X, Z, SWAP, DT_MID / 64>), dim3(gw), dim3(DT_BLOCK), 0,
-                                   gb_stream(), srf, sd, xv, yv, (Z *)tval, tflag, sseq);
+                                   gb_stream(), srf, info.mon, sd, xv, yv, (Z *)tval, tflag, sseq);
             // lists longer than the cap run as pieces of cap keys (4- and 8-byte results:
             // the pieces of an entry fold into its output slot with atomics)
             const bool pieces = (sizeof(Z) == 4 || sizeof(Z) == 8) && gb_knob("dot_pieces") != 1;
