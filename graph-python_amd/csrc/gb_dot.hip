@@ -572,7 +572,7 @@ constexpr int DT_SU = 4;
 // the entries' prefix -- so short Y lists no longer leave most of a wave idle; a hit (a few % of
 // the keys in these classes) folds into its entry's LDS slot by an atomic, so there is no
 // segmented scan.  Used with four keys per lane; seq 1: one entry at a time (A/B).
-constexpr int DT_FU = 4;
+constexpr int DT_FU = 2;  // steps of 64 keys in flight (4: 96 VGPRs; 2 measured 4 % faster at s20)
 
 template <class SR, class X, class Z, bool SWAP, int KPL>
 __global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, int mon, dt_side s, dt_vals<X> xvx, dt_vals<X> yvx,
