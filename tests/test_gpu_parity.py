@@ -963,3 +963,36 @@ def test_masked_dot_narrow_values(gb, lo, hi, dt):
                 gb.set_knob("narrow", 0)
         for Cg in got:
             _check_mat(Cg, ref)
+
+
+@pytest.mark.parametrize("knobs", [{}, {"dot_ypack": 1}, {"dot_xlds": 1}, {"dot_ypack": 1, "dot_xlds": 1},
+                                   {"dot_small_seq": 1}])
+@pytest.mark.parametrize("lo,hi", [(1, 256), (-128, 128), (0, 1 << 20)])
+def test_masked_dot_round6_value_paths(gb, knobs, lo, hi):
+    """Round 6's dot paths (gb_dot.hip): one-byte X values staged in LDS (knob dot_xlds = 1: off),
+    one-byte Y values packed into the streamed keys' top byte (dot_ypack = 1: off), the flat
+    small groups with LDS-slot folds (dot_small_seq = 1: the one-entry-at-a-time loop); unsigned,
+    signed and wider-than-a-byte values (the byte paths must stand aside), min.plus, plus.times
+    and max.plus, bit-exact vs the oracle under every knob setting."""
+    rng = np.random.default_rng(abs(lo) + hi % 977)
+    n = 1500
+    S = _skewed_both(rng, n, "BOOL")
+    r, c, _ = S.to_coo()
+    v = rng.integers(lo, hi, r.size, dtype=np.int64)
+    Ao = O.Csr.from_coo(r, c, v, nrows=n, ncols=n, dtype="INT64")
+    import ctypes
+
+    def stat(nm):
+        c = ctypes.c_int64()
+        assert gb.lib.GxB_Global_get_int(f"stat_{nm}".encode(), ctypes.byref(c)) == 0
+        return c.value
+
+    t0 = stat("dot_task_entries_R") + stat("dot_task_entries_C")
+    with _knobs(gb, **knobs):
+        Ag = _to_gb(gb, Ao)  # a fresh matrix: its narrow copies are built under these knobs
+        for name, mon, mul in (("min_plus", "MIN", "PLUS"), ("plus_times", "PLUS", "TIMES"),
+                               ("max_plus", "MAX", "PLUS")):
+            sr = getattr(gb.semiring, name)["INT64"]
+            ref = O.mxm(O.Csr.empty(n, n, "INT64"), Ao, Ao, (mon, mul, "INT64"), mask=Ao, mask_struct=True)
+            _check_mat(Ag.mxm(Ag, sr).new(mask=Ag.S), ref)
+    assert stat("dot_task_entries_R") + stat("dot_task_entries_C") > t0  # the task kernel ran
