@@ -556,22 +556,14 @@ __device__ __forceinline__ int dt_small_find(const int32_t (&xk)[KPL], int32_t y
     return pos;
 }
 
-__device__ __forceinline__ int64_t dt_readlane64(int64_t v, int t) {
-    const int lo = __builtin_amdgcn_readlane((int)(v & 0xffffffff), t);
-    const int hi = __builtin_amdgcn_readlane((int)(v >> 32), t);
-    return (int64_t)(uint32_t)lo | ((int64_t)hi << 32);
-}
 
-// entries of a small group taken DT_SU at a time (round 6): their first 64 Y keys are loaded
-// together, then searched, then the hits' values loaded together -- one entry at a time left
-// every wave waiting on a key load, a dependent shuffle search and a value load per entry
-constexpr int DT_SU = 4;
 
 // Flat entries (round 6, the default): a batch's entries' Y lists are one flat run of keys, 64 per
 // lane-step and DT_FU steps at a time -- a lane finds its element's entry by a shuffle search over
 // the entries' prefix -- so short Y lists no longer leave most of a wave idle; a hit (a few % of
 // the keys in these classes) folds into its entry's LDS slot by an atomic, so there is no
-// segmented scan.  Used with four keys per lane; seq 1: one entry at a time (A/B).
+// segmented scan (round 6: it replaced a loop taking four entries at a time, each a whole 64-lane
+// pass).  seq 1: one entry at a time (A/B).
 constexpr int DT_FU = 2;  // steps of 64 keys in flight (4: 96 VGPRs; 2 measured 4 % faster at s20)
 
 template <class SR, class X, class Z, bool SWAP, int KPL>
@@ -601,9 +593,8 @@ __global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, int mon, dt_side 
         // X's values: read on a hit from the row just loaded (an L2 hit); round 4 held them in
         // registers beside the keys and shuffled KPL of them (two 32-bit shuffles each for 8-byte
         // values) for every 64 Y keys -- the kernel is bound by its shuffles, not by these loads
-        // four keys per lane (X of 65..256 keys): flat entries; one key per lane: DT_SU entries at a
-        // time (measured: the flat form wins with four keys per lane and loses with one)
-        if (KPL > 1 && !seq) {
+        // flat entries for both classes (X of 1..64 and 65..256 keys; 64 / 72 VGPRs)
+        if (!seq) {
             for (int64_t pb = p0; pb < p1; pb += 64) {
                 const int nb = __builtin_amdgcn_readfirstlane((int)std::min<int64_t>(64, p1 - pb));
                 int32_t o_l = 0;
@@ -671,85 +662,6 @@ __global__ __launch_bounds__(DT_BLOCK) void k_dot_small(SR sr, int mon, dt_side 
                     tflag[q] = 1;
                 }
                 gb_wave_sync();  // the slots are rewritten by the next batch
-            }
-            continue;
-        }
-        if (KPL == 1 && !seq) {
-            for (int64_t pb = p0; pb < p1; pb += 64) {
-                const int nb = __builtin_amdgcn_readfirstlane((int)std::min<int64_t>(64, p1 - pb));
-                int32_t o_l = 0;
-                int64_t ys_l = 0;
-                int b_l = 0;
-                if (lane < nb) {
-                    o_l = s.grp_oi[pb + lane];
-                    ys_l = s.yrp[o_l];
-                    b_l = (int)(s.yrp[o_l + 1] - ys_l);
-                }
-                unsigned long long todo = __ballot(lane < nb && b_l > 0 && dt_side_of<SWAP>(a, b_l));
-                while (todo) {
-                    int tt[DT_SU], bb[DT_SU];
-                    int64_t yss[DT_SU];
-#pragma unroll
-                    for (int u = 0; u < DT_SU; u++) {
-                        tt[u] = 0;
-                        bb[u] = 0;
-                        yss[u] = 0;
-                        if (todo) {
-                            const int t = __builtin_ctzll(todo);
-                            todo &= todo - 1;
-                            tt[u] = t;
-                            bb[u] = __builtin_amdgcn_readlane(b_l, t);
-                            yss[u] = dt_readlane64(ys_l, t);
-                        }
-                    }
-                    int32_t yk[DT_SU];
-#pragma unroll
-                    for (int u = 0; u < DT_SU; u++) yk[u] = lane < bb[u] ? s.yci[yss[u] + lane] : -1;
-                    int pos[DT_SU];
-#pragma unroll
-                    for (int u = 0; u < DT_SU; u++) pos[u] = dt_small_find<KPL>(xk, yk[u], lane < bb[u]);
-                    X xm[DT_SU], yv[DT_SU];
-#pragma unroll
-                    for (int u = 0; u < DT_SU; u++) {
-                        xm[u] = yv[u] = X();
-                        if (rv && pos[u] >= 0) {
-                            xm[u] = xvx[xs + pos[u]];
-                            yv[u] = yvx[yss[u] + lane];
-                        }
-                    }
-#pragma unroll
-                    for (int u = 0; u < DT_SU; u++) {
-                        if (bb[u] == 0) continue;  // wave-uniform
-                        const int32_t o = __builtin_amdgcn_readlane(o_l, tt[u]);
-                        bool found = pos[u] >= 0;
-                        Z acc = found ? dt_mult<SR, X, Z, SWAP>(sr, xm[u], yv[u], g, yk[u], o) : Z();
-                        // keys past the first 64 (|Y| <= 64 * KPL): one chunk at a time
-                        for (int f0 = 64; f0 < bb[u]; f0 += 64) {
-                            const bool act = f0 + lane < bb[u];
-                            const int32_t k2 = act ? s.yci[yss[u] + f0 + lane] : -1;
-                            const int p2 = dt_small_find<KPL>(xk, k2, act);
-                            if (p2 >= 0) {
-                                X x2 = X(), y2 = X();
-                                if (rv) {
-                                    x2 = xvx[xs + p2];
-                                    y2 = yvx[yss[u] + f0 + lane];
-                                }
-                                const Z z = dt_mult<SR, X, Z, SWAP>(sr, x2, y2, g, k2, o);
-                                acc = found ? sr.add(acc, z) : z;
-                                found = true;
-                            }
-                        }
-                        if (__ballot(found)) {
-                            dt_wave_fold(sr, found, acc);
-                            if (lane == 0) {
-                                const int64_t p = pb + tt[u];
-                                const int64_t q = s.perm ? s.perm[p] : p;
-                                tval[q] = acc;
-                                tflag[q] = 1;
-                            }
-                        }
-                    }
-                }
             }
             continue;
         }
